@@ -1,0 +1,121 @@
+/*
+ * gdino_amd.h — C-ABI of the MI355X-native Grounding DINO hot path.
+ *
+ * Every entry point takes plain device pointers, sizes and a HIP stream
+ * (gd_stream_t is layout-compatible with hipStream_t; pass NULL for the null
+ * stream).  No torch types cross this boundary: the Python host side hands
+ * over tensor.data_ptr() and torch.cuda.current_stream().cuda_stream.
+ *
+ * Status convention (replaces the reference's printf-only launch errors,
+ * ops/src/cuda/ms_deform_im2col_cuda.cuh:948-952 and :1321-1325): every call
+ * returns GD_OK or an error code, and gd_last_error() gives the message of the
+ * most recent failure on the calling thread.
+ *
+ * Entry points and the reference interface each one replaces:
+ *
+ *   gd_msda_forward   <- ms_deform_attn_forward
+ *                        models/GroundingDINO/ops/src/vision.cpp:14,
+ *                        ops/src/ms_deform_attn.h:21-39,
+ *                        ops/src/cuda/ms_deform_attn_cuda.cu:20-80
+ *   gd_msda_backward  <- ms_deform_attn_backward
+ *                        models/GroundingDINO/ops/src/vision.cpp:15,
+ *                        ops/src/ms_deform_attn.h:41-61,
+ *                        ops/src/cuda/ms_deform_attn_cuda.cu:83-153
+ *   gd_runtime_info   <- get_cuda_version
+ *                        models/GroundingDINO/csrc/vision.cpp:11-51,
+ *                        models/GroundingDINO/csrc/cuda_version.cu
+ *   gd_window_attn_*  <- WindowAttention.forward core (q*scale@k^T + rel-pos
+ *                        bias + shift mask, softmax, @v)
+ *                        models/GroundingDINO/backbone/swin_transformer.py:134-174
+ *   gd_attn_*         <- scaled-dot-product attention with additive mask, used
+ *                        by BERT self-attention (bertwarper.py:141-152 via HF
+ *                        BertSelfAttention), the text enhancer
+ *                        (transformer_vanilla.py:101-123) and the decoder
+ *                        self / text cross attention (transformer.py:907-920)
+ *   gd_biattn_*       <- BiMultiHeadAttention.forward core
+ *                        models/GroundingDINO/fuse_modules.py:162-246
+ *   gd_contrastive_*  <- ContrastiveEmbed.forward
+ *                        models/GroundingDINO/utils.py:242-273
+ */
+#ifndef GDINO_AMD_H
+#define GDINO_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* gd_stream_t;
+
+typedef enum {
+  GD_OK = 0,
+  GD_ERR_INVALID = 1,     /* bad argument (shape, null pointer, dtype) */
+  GD_ERR_UNSUPPORTED = 2, /* valid but not implemented combination */
+  GD_ERR_LAUNCH = 3,      /* HIP launch / runtime error */
+} gd_status;
+
+typedef enum {
+  GD_F32 = 0,
+  GD_F64 = 1,
+  GD_BF16 = 2,
+  GD_F16 = 3,
+} gd_dtype;
+
+/* ------------------------------------------------------------------------ */
+/* Multi-scale deformable attention                                          */
+/* ------------------------------------------------------------------------ */
+/*
+ * value            [N, S, M, D]        value_dtype (F32, F64, BF16)
+ * spatial_shapes   [L, 2] int64 (H, W), device memory
+ * level_start_index[L]    int64,        device memory
+ * sampling_loc     [N, Lq, M, L, P, 2] loc_dtype = F64 if value is F64, else F32
+ * attn_weight      [N, Lq, M, L, P]    loc_dtype
+ * output           [N, Lq, M*D]        value_dtype; fully overwritten
+ *
+ * Semantics: ms_deformable_im2col_gpu_kernel, ms_deform_im2col_cuda.cuh:238-299
+ * (sample at loc*(W,H) - 0.5, bilinear, zero outside -1 < h < H, -1 < w < W).
+ */
+gd_status gd_msda_forward(gd_dtype value_dtype, const void* value,
+                          const int64_t* spatial_shapes,
+                          const int64_t* level_start_index,
+                          const void* sampling_loc, const void* attn_weight,
+                          int batch, int spatial_size, int num_heads,
+                          int channels, int num_levels, int num_query,
+                          int num_point, void* output, gd_stream_t stream);
+
+/*
+ * grad_output      [N, Lq, M*D]        value_dtype
+ * grad_value       [N, S, M, D]        accumulation dtype: F64 for F64 value,
+ *                                      else F32 (zeroed by this call)
+ * grad_sampling_loc[N, Lq, M, L, P, 2] loc_dtype (fully overwritten)
+ * grad_attn_weight [N, Lq, M, L, P]    loc_dtype (fully overwritten)
+ *
+ * Semantics: ms_deform_attn_col2im_bilinear, ms_deform_im2col_cuda.cuh:88-159.
+ * grad_value is accumulated with float atomics, so its low bits depend on
+ * arrival order (as in the reference).
+ */
+gd_status gd_msda_backward(gd_dtype value_dtype, const void* value,
+                           const int64_t* spatial_shapes,
+                           const int64_t* level_start_index,
+                           const void* sampling_loc, const void* attn_weight,
+                           const void* grad_output, int batch,
+                           int spatial_size, int num_heads, int channels,
+                           int num_levels, int num_query, int num_point,
+                           void* grad_value, void* grad_sampling_loc,
+                           void* grad_attn_weight, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Runtime                                                                   */
+/* ------------------------------------------------------------------------ */
+const char* gd_last_error(void);
+/* "hip=<runtime version>;arch=<gcnArchName of current device>;build=<hipcc>" */
+const char* gd_runtime_info(void);
+/* ABI version: bumped when a signature changes. */
+int gd_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDINO_AMD_H */

@@ -1,0 +1,72 @@
+// Shared helpers for the gfx950 kernels behind include/gdino_amd.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+
+#include "../../include/gdino_amd.h"
+
+namespace gd {
+
+// Per-thread message of the last failing call (gd_last_error()).
+void set_error(const char* fmt, ...);
+
+#define GD_REQUIRE(cond, ...)          \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::gd::set_error(__VA_ARGS__);    \
+      return GD_ERR_INVALID;           \
+    }                                  \
+  } while (0)
+
+#define GD_HIP_CHECK(expr)                                                    \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      ::gd::set_error("%s failed: %s", #expr, hipGetErrorString(_e));         \
+      return GD_ERR_LAUNCH;                                                   \
+    }                                                                         \
+  } while (0)
+
+// After a <<<>>> launch: surface launch-configuration errors as a status.
+#define GD_LAUNCH_CHECK(name)                                                 \
+  do {                                                                        \
+    hipError_t _e = hipGetLastError();                                        \
+    if (_e != hipSuccess) {                                                   \
+      ::gd::set_error("launch of %s failed: %s", name, hipGetErrorString(_e)); \
+      return GD_ERR_LAUNCH;                                                   \
+    }                                                                         \
+  } while (0)
+
+inline hipStream_t as_hip(gd_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- bf16 helpers (bit-level; the round-to-nearest-even store goes through
+// the __bf16 cast, which hipcc lowers to v_cvt_pk_bf16_f32 on gfx950 and which
+// keeps NaN a NaN) -----------------------------------------------------------
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+// ---- DPP lane exchange inside 8/16-lane groups ----------------------------
+// quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), row_half_mirror (i <-> 7-i),
+// row_ror:8 (i <-> i^8 inside a 16-lane row).
+enum : int {
+  DPP_XOR1 = 0xB1,
+  DPP_XOR2 = 0x4E,
+  DPP_HALF_MIRROR = 0x141,
+  DPP_ROR8 = 0x128,
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_amdgcn_update_dpp(0.f, v, CTRL, 0xf, 0xf, false);
+}
+
+}  // namespace gd

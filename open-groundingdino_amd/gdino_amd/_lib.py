@@ -1,0 +1,127 @@
+"""ctypes binding of libgdino_amd.so (the C-ABI declared in include/gdino_amd.h).
+
+This is the only door from Python into the HIP kernels.  There is no CPU or
+eager-PyTorch fallback behind it: if the library is missing, or a tensor is
+not on a ROCm device, the call raises — mirroring the reference extension,
+whose CPU backend raises "Not implemented on the CPU"
+(models/GroundingDINO/ops/src/ms_deform_attn.h:38,60).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GDINO_AMD_LIB", os.path.join(_HERE, "lib", "libgdino_amd.so"))
+
+GD_OK, GD_ERR_INVALID, GD_ERR_UNSUPPORTED, GD_ERR_LAUNCH = 0, 1, 2, 3
+GD_F32, GD_F64, GD_BF16, GD_F16 = 0, 1, 2, 3
+
+_DTYPE_CODE = {
+    torch.float32: GD_F32,
+    torch.float64: GD_F64,
+    torch.bfloat16: GD_BF16,
+    torch.float16: GD_F16,
+}
+
+_lock = threading.Lock()
+_lib = None
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+# name -> (argtypes) ; every function returns gd_status (int)
+_SIGNATURES = {
+    "gd_msda_forward": [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p],
+    "gd_msda_backward": [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p],
+}
+
+
+class GdError(RuntimeError):
+    """A C-ABI call returned a non-OK gd_status."""
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"gdino_amd: HIP library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C "
+                "open-groundingdino_amd/csrc)"
+            )
+        # torch must own the HIP runtime first so the library binds to it
+        # (same soname libamdhip64.so.7) and torch's streams stay valid.
+        import torch.cuda  # noqa: F401
+
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        handle.gd_last_error.restype = ctypes.c_char_p
+        handle.gd_runtime_info.restype = ctypes.c_char_p
+        handle.gd_abi_version.restype = ctypes.c_int
+        if handle.gd_abi_version() != 1:
+            raise RuntimeError("gdino_amd: ABI version mismatch")
+        _lib = handle
+        return _lib
+
+
+def register(name: str, argtypes) -> None:
+    """Declare the signature of an additional entry point (used by kernel
+    modules that extend the ABI)."""
+    _SIGNATURES[name] = argtypes
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+
+
+def call(name: str, *args) -> None:
+    status = getattr(lib(), name)(*args)
+    if status != GD_OK:
+        msg = lib().gd_last_error().decode(errors="replace")
+        raise GdError(f"{name}: status {status}: {msg}")
+
+
+def runtime_info() -> str:
+    return lib().gd_runtime_info().decode()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DTYPE_CODE[t.dtype]
+    except KeyError:
+        raise TypeError(f"gdino_amd: unsupported dtype {t.dtype}") from None
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_device(*tensors: torch.Tensor, what: str = "op") -> None:
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(f"gdino_amd {what}: Not implemented on the CPU (tensor on {t.device})")
+
+
+def require_contiguous(what: str, **tensors: torch.Tensor) -> None:
+    for name, t in tensors.items():
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError(f"{name} tensor has to be contiguous ({what})")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()

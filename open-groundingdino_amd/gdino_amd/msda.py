@@ -1,0 +1,96 @@
+"""Op-level MSDA API: a drop-in for the reference extension module
+``MultiScaleDeformableAttention`` (models/GroundingDINO/ops/src/vision.cpp:13-16),
+backed by the HIP kernels of csrc/msda.hip through the C-ABI.
+
+Contract kept from ops/src/cuda/ms_deform_attn_cuda.cu:20-153:
+  * inputs must be contiguous device tensors, else RuntimeError;
+  * ``batch % min(batch, im2col_step) == 0`` else RuntimeError;
+  * outputs are freshly allocated and owned by the caller;
+  * work is enqueued on the current stream.
+Differences (documented in DESIGN.md): the whole batch is one launch (no
+im2col_step chunking — it only bounded the reference's column buffer), bf16
+``value`` is accepted (fp32 accumulate; sampling locations / weights stay
+fp32), and launch errors raise instead of being printed.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _acc_dtype(value: torch.Tensor) -> torch.dtype:
+    return torch.float64 if value.dtype == torch.float64 else torch.float32
+
+
+def _check(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, im2col_step, extra=()):
+    _lib.require_device(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, *extra,
+                        what="ms_deform_attn")
+    _lib.require_contiguous("ms_deform_attn", value=value, spatial_shapes=spatial_shapes,
+                            level_start_index=level_start_index, sampling_loc=sampling_loc,
+                            attn_weight=attn_weight)
+    if value.dim() != 4:
+        raise RuntimeError(f"value must be [N, S, M, D], got {tuple(value.shape)}")
+    N, S, M, D = value.shape
+    if sampling_loc.dim() != 6 or sampling_loc.size(-1) != 2:
+        raise RuntimeError(f"sampling_loc must be [N, Lq, M, L, P, 2], got {tuple(sampling_loc.shape)}")
+    L = spatial_shapes.size(0)
+    _, Lq, M2, L2, P, _ = sampling_loc.shape
+    if sampling_loc.size(0) != N or M2 != M or L2 != L:
+        raise RuntimeError("sampling_loc shape does not match value / spatial_shapes")
+    if tuple(attn_weight.shape) != (N, Lq, M, L, P):
+        raise RuntimeError(f"attn_weight must be {(N, Lq, M, L, P)}, got {tuple(attn_weight.shape)}")
+    if spatial_shapes.dtype != torch.int64 or level_start_index.dtype != torch.int64:
+        raise RuntimeError("spatial_shapes / level_start_index must be int64")
+    step = min(N, int(im2col_step)) if N > 0 else 1
+    if step <= 0 or N % step != 0:
+        raise RuntimeError(f"batch({N}) must divide im2col_step({step})")
+    acc = _acc_dtype(value)
+    if sampling_loc.dtype != acc:
+        sampling_loc = sampling_loc.to(acc).contiguous()
+    if attn_weight.dtype != acc:
+        attn_weight = attn_weight.to(acc).contiguous()
+    return (N, S, M, D, L, Lq, P), sampling_loc, attn_weight
+
+
+def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                           im2col_step: int = 64) -> torch.Tensor:
+    """-> output [N, Lq, M*D] (value dtype)."""
+    (N, S, M, D, L, Lq, P), loc, attn = _check(value, spatial_shapes, level_start_index,
+                                               sampling_loc, attn_weight, im2col_step)
+    out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+    _lib.call("gd_msda_forward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
+              level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), N, S, M, D, L, Lq, P,
+              out.data_ptr(), _lib.stream_of(value))
+    return out
+
+
+def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                            grad_output, im2col_step: int = 64, grad_value_dtype=None):
+    """-> [grad_value, grad_sampling_loc, grad_attn_weight].
+
+    grad_value is accumulated in fp32 (fp64 for fp64 value); it is returned in
+    ``grad_value_dtype`` (default: value.dtype, as the reference)."""
+    (N, S, M, D, L, Lq, P), loc, attn = _check(value, spatial_shapes, level_start_index,
+                                               sampling_loc, attn_weight, im2col_step,
+                                               extra=(grad_output,))
+    if grad_output.dtype != value.dtype:
+        grad_output = grad_output.to(value.dtype)
+    grad_output = grad_output.contiguous()
+    if grad_output.numel() != N * Lq * M * D:
+        raise RuntimeError("grad_output must be [N, Lq, M*D]")
+    acc = _acc_dtype(value)
+    grad_value = torch.empty((N, S, M, D), dtype=acc, device=value.device)
+    grad_loc = torch.empty((N, Lq, M, L, P, 2), dtype=acc, device=value.device)
+    grad_attn = torch.empty((N, Lq, M, L, P), dtype=acc, device=value.device)
+    _lib.call("gd_msda_backward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
+              level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), grad_output.data_ptr(),
+              N, S, M, D, L, Lq, P, grad_value.data_ptr(), grad_loc.data_ptr(), grad_attn.data_ptr(),
+              _lib.stream_of(value))
+    out_dtype = value.dtype if grad_value_dtype is None else grad_value_dtype
+    if grad_value.dtype != out_dtype:
+        grad_value = grad_value.to(out_dtype)
+    if grad_loc.dtype != sampling_loc.dtype:
+        grad_loc = grad_loc.to(sampling_loc.dtype)
+        grad_attn = grad_attn.to(attn_weight.dtype)
+    return [grad_value, grad_loc, grad_attn]

@@ -1,0 +1,4 @@
+"""Reference-compatible model package: ``models.registry.MODULE_BUILD_FUNCS``
+and ``models.GroundingDINO.build_groundingdino`` (reference models/__init__.py,
+models/registry.py), so the reference's main.py/engines import this package
+unchanged once ``open-groundingdino_amd/`` is on sys.path."""

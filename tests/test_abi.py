@@ -1,0 +1,62 @@
+"""CPU-side checks of the C-ABI boundary: the shared library exists, loads,
+and exports every entry point declared in include/gdino_amd.h (no compute
+calls — there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "gdino_amd.h")
+LIB = os.path.join(PKG, "gdino_amd", "lib", "libgdino_amd.so")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gd_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_core_entry_points():
+    syms = declared_symbols()
+    for s in ("gd_msda_forward", "gd_msda_backward", "gd_last_error", "gd_runtime_info",
+              "gd_abi_version"):
+        assert s in syms
+
+
+def test_library_built_and_exports_header():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    lib = ctypes.CDLL(LIB)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    lib.gd_abi_version.restype = ctypes.c_int
+    assert lib.gd_abi_version() == 1
+
+
+def test_library_targets_gfx950_only():
+    blob = open(LIB, "rb").read()
+    assert b"gfx950" in blob
+    for other in (b"gfx942", b"gfx90a", b"gfx1100"):
+        assert other not in blob
+
+
+def test_python_binding_signatures_cover_header():
+    from gdino_amd import _lib
+    compute = [s for s in declared_symbols()
+               if s not in ("gd_last_error", "gd_runtime_info", "gd_abi_version")]
+    missing = [s for s in compute if s not in _lib._SIGNATURES]
+    assert not missing, missing
+
+
+def test_product_refuses_cpu_tensors():
+    import torch
+    from gdino_amd import msda
+    v = torch.zeros(1, 4, 1, 2)
+    shapes = torch.tensor([[2, 2]])
+    lsi = torch.tensor([0])
+    loc = torch.zeros(1, 1, 1, 1, 1, 2)
+    attn = torch.ones(1, 1, 1, 1, 1)
+    with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
+        msda.ms_deform_attn_forward(v, shapes, lsi, loc, attn, 64)
