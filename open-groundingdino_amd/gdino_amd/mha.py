@@ -1,0 +1,107 @@
+"""Multi-head attention with nn.MultiheadAttention's parameter layout
+(``in_proj_weight``, ``in_proj_bias``, ``out_proj``) and call contract
+(sequence-first by default, bool masks True = "not allowed", float masks
+additive, ``attn_mask`` [L, S] or [B*H, L, S] in batch-major (b*H + h) order,
+``key_padding_mask`` [B, S] True = pad), whose core runs through
+``gdino_amd.kernels.attention``.  Used where the reference instantiates
+nn.MultiheadAttention on the hot path: the text enhancer
+(transformer_vanilla.py:83) and the decoder self / text-cross attention
+(transformer.py:839,844).  Returns (output, None): attention weights are never
+requested on the hot path."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+
+def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor], b: int, h: int,
+                lq: int, lk: int, dtype) -> Optional[Tensor]:
+    """-> bool keep-mask or float additive mask broadcastable to [B, H, Lq, Lk]."""
+    if attn_mask is None and key_padding_mask is None:
+        return None
+    am = None
+    if attn_mask is not None:
+        am = attn_mask
+        if am.dim() == 2:
+            am = am.view(1, 1, lq, lk)
+        elif am.dim() == 3:
+            am = am.view(b, h, lq, lk)
+    kp = None
+    if key_padding_mask is not None:
+        kp = key_padding_mask.view(b, 1, 1, lk)
+    floats = [m for m in (am, kp) if m is not None and m.dtype != torch.bool]
+    if not floats:
+        keep = None
+        if am is not None:
+            keep = ~am
+        if kp is not None:
+            keep = ~kp if keep is None else keep & ~kp
+        return keep
+    add = torch.zeros((), dtype=dtype, device=(am if am is not None else kp).device)
+    for m in (am, kp):
+        if m is None:
+            continue
+        if m.dtype == torch.bool:
+            add = add + torch.zeros_like(m, dtype=dtype).masked_fill(m, float("-inf"))
+        else:
+            add = add + m.to(dtype)
+    return add
+
+
+class MultiheadAttention(nn.Module):
+    def __init__(self, embed_dim, num_heads, dropout=0.0, bias=True, batch_first=False):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.num_heads = num_heads
+        self.head_dim = embed_dim // num_heads
+        assert self.head_dim * num_heads == embed_dim, "embed_dim must be divisible by num_heads"
+        self.dropout = dropout
+        self.batch_first = batch_first
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
+        self.in_proj_bias = nn.Parameter(torch.empty(3 * embed_dim)) if bias else None
+        self.out_proj = nn.Linear(embed_dim, embed_dim, bias=bias)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        if self.in_proj_bias is not None:
+            nn.init.constant_(self.in_proj_bias, 0.0)
+            nn.init.constant_(self.out_proj.bias, 0.0)
+
+    def _project(self, query, key, value):
+        e = self.embed_dim
+        w, bias = self.in_proj_weight, self.in_proj_bias
+        if query is key and key is value:
+            return F.linear(query, w, bias).chunk(3, dim=-1)
+        bq, bk, bv = (None, None, None) if bias is None else bias.split(e)
+        wq, wk, wv = w.split(e)
+        q = F.linear(query, wq, bq)
+        if key is value:
+            k, v = F.linear(key, torch.cat([wk, wv]), None if bias is None else torch.cat([bk, bv])).chunk(2, -1)
+        else:
+            k, v = F.linear(key, wk, bk), F.linear(value, wv, bv)
+        return q, k, v
+
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=False, attn_mask=None,
+                average_attn_weights=True, is_causal=False):
+        from . import kernels
+        if self.batch_first:
+            query, key, value = (x.transpose(0, 1) for x in (query, key, value))
+        lq, b, e = query.shape
+        lk = key.shape[0]
+        q, k, v = self._project(query, key, value)
+        h, hd = self.num_heads, self.head_dim
+        # [L, B, E] -> [B, H, L, hd]
+        q = q.view(lq, b, h, hd).permute(1, 2, 0, 3)
+        k = k.view(lk, b, h, hd).permute(1, 2, 0, 3)
+        v = v.view(lk, b, h, hd).permute(1, 2, 0, 3)
+        mask = merge_masks(attn_mask, key_padding_mask, b, h, lq, lk, q.dtype)
+        out = kernels.attention(q, k, v, mask, None, self.dropout if self.training else 0.0)
+        out = out.permute(2, 0, 1, 3).reshape(lq, b, e)
+        out = self.out_proj(out)
+        if self.batch_first:
+            out = out.transpose(0, 1)
+        return out, None

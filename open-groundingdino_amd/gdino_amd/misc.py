@@ -1,0 +1,139 @@
+"""Small host-side utilities the model needs (the reference pulls them from
+groundingdino/util/misc.py and timm): NestedTensor, padding of image lists,
+inverse_sigmoid, distributed helpers, DropPath, trunc_normal_."""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+from torch import Tensor, nn
+
+
+class NestedTensor:
+    """Batched images + padding mask (True on padded pixels).
+    Contract of groundingdino/util/misc.py:399-480; the model also accepts any
+    object with ``.tensors`` and ``.mask`` (e.g. the reference's own class)."""
+
+    def __init__(self, tensors: Tensor, mask: Optional[Tensor]):
+        self.tensors = tensors
+        self.mask = mask
+
+    def to(self, device, non_blocking=False):
+        m = None if self.mask is None else self.mask.to(device, non_blocking=non_blocking)
+        return NestedTensor(self.tensors.to(device, non_blocking=non_blocking), m)
+
+    def decompose(self):
+        return self.tensors, self.mask
+
+    @property
+    def device(self):
+        return self.tensors.device
+
+    @property
+    def shape(self):
+        return {"tensors.shape": self.tensors.shape, "mask.shape": self.mask.shape}
+
+    def __repr__(self):
+        return f"NestedTensor(tensors={tuple(self.tensors.shape)}, mask={None if self.mask is None else tuple(self.mask.shape)})"
+
+
+def nested_tensor_from_tensor_list(tensor_list) -> NestedTensor:
+    """Zero-pad [C,H,W] images to the batch max size; mask marks the padding
+    (groundingdino/util/misc.py:483-506)."""
+    if isinstance(tensor_list, Tensor) and tensor_list.dim() == 4:
+        b, _, h, w = tensor_list.shape
+        return NestedTensor(tensor_list, torch.zeros((b, h, w), dtype=torch.bool, device=tensor_list.device))
+    if tensor_list[0].ndim != 3:
+        raise ValueError("not supported")
+    c = max(t.shape[0] for t in tensor_list)
+    h = max(t.shape[1] for t in tensor_list)
+    w = max(t.shape[2] for t in tensor_list)
+    first = tensor_list[0]
+    batch = first.new_zeros((len(tensor_list), c, h, w))
+    mask = torch.ones((len(tensor_list), h, w), dtype=torch.bool, device=first.device)
+    for i, img in enumerate(tensor_list):
+        batch[i, : img.shape[0], : img.shape[1], : img.shape[2]].copy_(img)
+        mask[i, : img.shape[1], : img.shape[2]] = False
+    return NestedTensor(batch, mask)
+
+
+def inverse_sigmoid(x: Tensor, eps: float = 1e-3) -> Tensor:
+    """logit with clamping (groundingdino/util/misc.py:704-708)."""
+    x = x.clamp(min=0, max=1)
+    return torch.log(x.clamp(min=eps) / (1 - x).clamp(min=eps))
+
+
+def is_dist_avail_and_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if is_dist_avail_and_initialized() else 1
+
+
+def get_rank() -> int:
+    return dist.get_rank() if is_dist_avail_and_initialized() else 0
+
+
+def drop_path(x: Tensor, drop_prob: float = 0.0, training: bool = False) -> Tensor:
+    """Stochastic depth per sample (timm semantics: scale kept paths by 1/keep)."""
+    if drop_prob == 0.0 or not training:
+        return x
+    keep = 1.0 - drop_prob
+    shape = (x.shape[0],) + (1,) * (x.ndim - 1)
+    mask = x.new_empty(shape).bernoulli_(keep)
+    return x * mask.div_(keep)
+
+
+class DropPath(nn.Module):
+    def __init__(self, drop_prob: float = 0.0):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        return drop_path(x, self.drop_prob, self.training)
+
+    def extra_repr(self):
+        return f"drop_prob={self.drop_prob}"
+
+
+def trunc_normal_(tensor: Tensor, mean=0.0, std=1.0, a=-2.0, b=2.0) -> Tensor:
+    with torch.no_grad():
+        return nn.init.trunc_normal_(tensor, mean=mean, std=std, a=a, b=b)
+
+
+def to_2tuple(x):
+    return tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+
+
+def clean_state_dict(state_dict):
+    """Strip DDP's ``module.`` prefix (util/misc.py:620-626)."""
+    return {(k[7:] if k.startswith("module.") else k): v for k, v in state_dict.items()}
+
+
+def accuracy(output, target, topk=(1,)):
+    if target.numel() == 0:
+        return [torch.zeros([], device=output.device)]
+    maxk = max(topk)
+    _, pred = output.topk(maxk, 1, True, True)
+    correct = pred.t().eq(target.view(1, -1).expand_as(pred.t()))
+    return [correct[:k].reshape(-1).float().sum(0).mul_(100.0 / target.size(0)) for k in topk]
+
+
+def sigmoid_focal_loss(inputs, targets, num_boxes, alpha: float = 0.25, gamma: float = 2,
+                       no_reduction=False):
+    """RetinaNet focal loss (reference utils.py:152-181)."""
+    prob = inputs.sigmoid()
+    ce = nn.functional.binary_cross_entropy_with_logits(inputs, targets, reduction="none")
+    p_t = prob * targets + (1 - prob) * (1 - targets)
+    loss = ce * ((1 - p_t) ** gamma)
+    if alpha >= 0:
+        loss = (alpha * targets + (1 - alpha) * (1 - targets)) * loss
+    if no_reduction:
+        return loss
+    return loss.mean(1).sum() / num_boxes
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("math", "List", "Optional")]

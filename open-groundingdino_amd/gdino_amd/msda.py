@@ -19,6 +19,46 @@ import torch
 from . import _lib
 
 
+class LaunchTimer:
+    """Optional HIP-event bracketing of every MSDA launch (bench.py's live
+    roofline measurement).  Events are recorded on the launch stream (torch's
+    current stream, which is where the C-ABI call enqueues the kernel)."""
+
+    def __init__(self):
+        self.records = []  # (kind, lq, bytes, start_event, end_event)
+
+    def begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, kind, lq, nbytes, start):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.records.append((kind, lq, nbytes, start, ev))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, lq, nbytes, s, e in self.records:
+            d = out.setdefault((kind, lq), {"n": 0, "ms": 0.0, "bytes": nbytes})
+            d["n"] += 1
+            d["ms"] += s.elapsed_time(e)
+        return out
+
+
+timer = None  # set to a LaunchTimer to measure
+
+
+def algorithmic_bytes(kind, N, S, M, D, L, Lq, P, sv, sf=4, so=None):
+    """SURVEY §8d per-launch algorithmic traffic.  fwd: value + (loc, attn) +
+    out.  bwd: value + grad_value (fp32) + 2x(loc, attn, grads) + grad_out."""
+    so = sv if so is None else so
+    if kind == "fwd":
+        return sv * N * S * M * D + 3 * sf * N * Lq * M * L * P + so * N * Lq * M * D
+    return sv * N * S * M * D + 4 * N * S * M * D + 6 * sf * N * Lq * M * L * P + so * N * Lq * M * D
+
+
 def _acc_dtype(value: torch.Tensor) -> torch.dtype:
     return torch.float64 if value.dtype == torch.float64 else torch.float32
 
@@ -59,9 +99,12 @@ def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_lo
     (N, S, M, D, L, Lq, P), loc, attn = _check(value, spatial_shapes, level_start_index,
                                                sampling_loc, attn_weight, im2col_step)
     out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+    t0 = timer.begin() if timer is not None else None
     _lib.call("gd_msda_forward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
               level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), N, S, M, D, L, Lq, P,
               out.data_ptr(), _lib.stream_of(value))
+    if t0 is not None:
+        timer.end("fwd", Lq, algorithmic_bytes("fwd", N, S, M, D, L, Lq, P, value.element_size()), t0)
     return out
 
 
@@ -83,10 +126,13 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     grad_value = torch.empty((N, S, M, D), dtype=acc, device=value.device)
     grad_loc = torch.empty((N, Lq, M, L, P, 2), dtype=acc, device=value.device)
     grad_attn = torch.empty((N, Lq, M, L, P), dtype=acc, device=value.device)
+    t0 = timer.begin() if timer is not None else None
     _lib.call("gd_msda_backward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
               level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), grad_output.data_ptr(),
               N, S, M, D, L, Lq, P, grad_value.data_ptr(), grad_loc.data_ptr(), grad_attn.data_ptr(),
               _lib.stream_of(value))
+    if t0 is not None:
+        timer.end("bwd", Lq, algorithmic_bytes("bwd", N, S, M, D, L, Lq, P, value.element_size()), t0)
     out_dtype = value.dtype if grad_value_dtype is None else grad_value_dtype
     if grad_value.dtype != out_dtype:
         grad_value = grad_value.to(out_dtype)

@@ -1,0 +1,151 @@
+"""Training-step plumbing around the drop-in model: synthetic odvg batches,
+optimizer parameter groups, freezing, and one train step.
+
+Restates what the reference's main.py / engine_multi.py do around
+``model`` and ``criterion`` (main.py:254-292, engine_multi.py:499-564)
+without the PAVE crop tiling (product-specific, out of scope):
+  * freezing: names containing 'attn' stay trainable, then any name
+    containing a freeze keyword is frozen (main.py:269-281; 'bert' by cfg);
+  * AdamW over util/get_param_dicts.py 'ddetr_in_mmdet' groups (:34-53);
+  * autocast (bf16 here; the reference's --amp is fp16) -> model ->
+    criterion -> weighted sum -> backward -> clip_grad_norm_(0.1) -> step.
+"""
+from __future__ import annotations
+
+import random
+from typing import List, Tuple
+
+import torch
+
+from .misc import NestedTensor
+
+
+# ------------------------------------------------------------------ batches
+def _phrase_words(rng: random.Random, n_words: int, used: set) -> str:
+    while True:
+        words = [f"w{rng.randrange(10000, 99999)}" for _ in range(n_words)]
+        p = " ".join(words)
+        if p not in used:
+            used.add(p)
+            return p
+
+
+def synthetic_caption(rng: random.Random, n_tokens: int = 256) -> List[str]:
+    """Phrases whose caption ' . '.join(phrases) + ' .' tokenizes to exactly
+    n_tokens ([CLS] + words and '.' separators + [SEP]) with the offline
+    tokenizer (one token per word); phrase lengths 1-8 words."""
+    budget = n_tokens - 2  # CLS, SEP
+    phrases, used = [], set()
+    while budget > 0:
+        n = min(rng.randint(1, 8), budget - 1)
+        if n <= 0:
+            break
+        phrases.append(_phrase_words(rng, n, used))
+        budget -= n + 1  # words + '.'
+    if budget > 0:  # one token left over: lengthen the last phrase
+        phrases[-1] = phrases[-1] + f" w{rng.randrange(10000, 99999)}"
+    return phrases
+
+
+def synthetic_batch(bs: int, height: int, width: int, n_boxes: int = 8, n_tokens: int = 256, seed: int = 0,
+                    device="cuda", dtype=torch.float32) -> Tuple[NestedTensor, list, list, list]:
+    """-> (samples, targets, captions, cat_lists) shaped like an odvg batch
+    (datasets/odvg.py:254-260): boxes cxcywh normalised (centres U[0.2,0.8],
+    sizes U[0.05,0.3]), labels index the image's phrase list."""
+    rng = random.Random(seed)
+    g = torch.Generator().manual_seed(seed)
+    imgs = torch.randn(bs, 3, height, width, generator=g).to(device, dtype)
+    mask = torch.zeros(bs, height, width, dtype=torch.bool, device=device)
+    targets, captions, cat_lists = [], [], []
+    for i in range(bs):
+        cats = synthetic_caption(rng, n_tokens)
+        caption = " . ".join(cats) + " ."
+        labels = torch.randint(0, len(cats), (n_boxes,), generator=g)
+        ctr = torch.rand(n_boxes, 2, generator=g) * 0.6 + 0.2
+        wh = torch.rand(n_boxes, 2, generator=g) * 0.25 + 0.05
+        boxes = torch.cat([ctr, wh], -1)
+        targets.append({"boxes": boxes.to(device), "labels": labels.to(device), "caption": caption,
+                        "cap_list": cats, "size": torch.tensor([height, width], device=device),
+                        "orig_size": torch.tensor([height, width], device=device)})
+        captions.append(caption)
+        cat_lists.append(cats)
+    return NestedTensor(imgs, mask), targets, captions, cat_lists
+
+
+# --------------------------------------------------------------- optimizer
+def _match(name, keywords):
+    return any(k in name for k in keywords)
+
+
+def apply_freeze(args, model) -> None:
+    if getattr(args, "freeze_keywords", None) is None:
+        return
+    for name, p in model.named_parameters():
+        if "attn" in name:
+            p.requires_grad_(True)
+        elif _match(name, args.freeze_keywords):
+            p.requires_grad_(False)
+
+
+def get_param_dict(args, model):
+    """util/get_param_dicts.py:15-85 ('default' and 'ddetr_in_mmdet')."""
+    kind = getattr(args, "param_dict_type", "default")
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    if kind == "default":
+        return [{"params": [p for n, p in named if "backbone" not in n]},
+                {"params": [p for n, p in named if "backbone" in n], "lr": args.lr_backbone}]
+    if kind == "ddetr_in_mmdet":
+        bb, lp = args.lr_backbone_names, args.lr_linear_proj_names
+        return [
+            {"params": [p for n, p in named if not _match(n, bb) and not _match(n, lp)], "lr": args.lr},
+            {"params": [p for n, p in named if _match(n, bb)], "lr": args.lr_backbone},
+            {"params": [p for n, p in named if _match(n, lp)], "lr": args.lr_linear_proj_mult},
+        ]
+    raise ValueError(f"param_dict_type {kind} not supported")
+
+
+def build_optimizer(args, model):
+    groups = [g for g in get_param_dict(args, model) if g["params"]]
+    # fused AdamW: one multi-tensor launch chain instead of per-parameter ops
+    return torch.optim.AdamW(groups, lr=args.lr, weight_decay=args.weight_decay,
+                             fused=next(model.parameters()).is_cuda)
+
+
+# -------------------------------------------------------------------- step
+def train_step(model, criterion, optimizer, samples, targets, captions, cat_lists, clip_max_norm=0.1,
+               amp_dtype=torch.bfloat16):
+    """One optimisation step; returns the weighted loss tensor (not synced)."""
+    dev_type = samples.tensors.device.type
+    with torch.autocast(device_type=dev_type, dtype=amp_dtype, enabled=amp_dtype is not None):
+        outputs = model(samples, captions=captions)
+        loss_dict = criterion(outputs, targets, cat_lists, captions)
+        wd = criterion.weight_dict
+        loss = sum(loss_dict[k] * wd[k] for k in loss_dict if k in wd)
+    optimizer.zero_grad(set_to_none=True)
+    loss.backward()
+    if clip_max_norm > 0:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), clip_max_norm, foreach=True)
+    optimizer.step()
+    return loss.detach()
+
+
+def build_training(args, device):
+    from models.GroundingDINO import build_groundingdino
+    model, criterion, post = build_groundingdino(args)
+    model.to(device)
+    apply_freeze(args, model)
+    optimizer = build_optimizer(args, model)
+    return model, criterion, post, optimizer
+
+
+def small_train_step(device, height=256, width=320, seed=0) -> float:
+    """smoke(): one tiny train step of the full Swin-T + BERT-base model."""
+    from .config import make_args
+    torch.manual_seed(seed)
+    args = make_args(device=str(device))
+    model, criterion, _, opt = build_training(args, device)
+    model.train()
+    samples, targets, captions, cats = synthetic_batch(1, height, width, n_boxes=3, n_tokens=24, seed=seed,
+                                                       device=device)
+    loss = train_step(model, criterion, opt, samples, targets, captions, cats)
+    return float(loss)

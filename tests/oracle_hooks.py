@@ -1,0 +1,23 @@
+"""Test-only: run the model's host logic on CPU by routing the HIP-only MSDA
+op to the oracle restatement.  The product raises on CPU tensors; this hook
+is the only way CPU tests execute MSDA."""
+import contextlib
+
+from oracle.msda_torch import msda_gather
+
+
+class _OracleMSDA:
+    @staticmethod
+    def apply(value, shapes, lsi, loc, attn, im2col_step):
+        return msda_gather(value, shapes, lsi, loc.to(value.dtype), attn.to(value.dtype))
+
+
+@contextlib.contextmanager
+def oracle_msda():
+    import models.GroundingDINO.ms_deform_attn as mod
+    prev = mod.MSDeformAttnFunction
+    mod.MSDeformAttnFunction = _OracleMSDA
+    try:
+        yield
+    finally:
+        mod.MSDeformAttnFunction = prev
