@@ -125,7 +125,7 @@ class SwinTransformerBlock(nn.Module):
         hp, wp = h + pad_b, w + pad_r
         if sh > 0:
             x = torch.roll(x, shifts=(-sh, -sh), dims=(1, 2))
-        windows = window_partition(x, ws).view(-1, ws * ws, c)
+        windows = window_partition(x, ws).reshape(-1, ws * ws, c)
         windows = self.attn(windows, mask=mask_matrix if sh > 0 else None)
         x = window_reverse(windows.view(-1, ws, ws, c), ws, hp, wp)
         if sh > 0:
@@ -171,7 +171,7 @@ def shifted_window_mask(hp: int, wp: int, ws: int, shift: int, device) -> torch.
                 region[cuts[0][i]:cuts[0][i + 1], cuts[1][j]:cuts[1][j + 1]] = label
                 label += 1
         t = torch.from_numpy(region).view(1, hp, wp, 1)
-        win = window_partition(t, ws).view(-1, ws * ws)
+        win = window_partition(t, ws).reshape(-1, ws * ws)
         diff = win[:, None, :] - win[:, :, None]
         m = torch.where(diff != 0, torch.tensor(-100.0), torch.tensor(0.0)).to(device)
         _MASK_CACHE[key] = m

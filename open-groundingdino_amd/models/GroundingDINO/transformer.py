@@ -150,7 +150,7 @@ class Transformer(nn.Module):
         text_dict["encoded_text"] = memory_text
 
         if self.two_stage_type == "standard":
-            output_memory, output_proposals = gen_encoder_output_proposals(memory, mask_flatten, spatial_shapes)
+            output_memory, output_proposals = gen_encoder_output_proposals(memory, mask_flatten, shapes_list)
             output_memory = self.enc_output_norm(self.enc_output(output_memory))
             enc_cls = self.enc_out_class_embed(output_memory, text_dict)
             topk_logits = enc_cls.max(-1)[0]

@@ -61,7 +61,8 @@ def gen_encoder_output_proposals(memory: Tensor, memory_padding_mask: Tensor, sp
     n = memory.shape[0]
     proposals = []
     cur = 0
-    for lvl, (h, w) in enumerate(spatial_shapes.tolist()):
+    shapes = spatial_shapes.tolist() if torch.is_tensor(spatial_shapes) else spatial_shapes
+    for lvl, (h, w) in enumerate(shapes):
         m = memory_padding_mask[:, cur:cur + h * w].view(n, h, w)
         valid_h = (~m[:, :, 0]).sum(1).float()
         valid_w = (~m[:, 0, :]).sum(1).float()

@@ -1,0 +1,101 @@
+"""oracle/blocks.py — TEST INFRASTRUCTURE ONLY.
+
+Literal CPU restatements (plain torch, materialising every intermediate the
+way the reference does) of the attention-family ops that the product routes
+through fused kernels.  Tests compare the product's kernels against these,
+and these are pinned against reference-generated fixtures where the
+reference module imports here (tests/golden/make_block_golden.py).
+
+  bi_attention_ref     fuse_modules.py:162-246 (global max shift, +-5e4
+                       clamps, column-max shift, -inf masks, two softmaxes)
+  window_attention_ref swin_transformer.py:134-174
+  attention_ref        masked softmax(q k^T * scale) v (additive / bool mask)
+  contrastive_ref      utils.py:242-273
+  phrase_masks_ref     bertwarper.py:224-273 (per-special-token loop)
+"""
+from __future__ import annotations
+
+import torch
+
+
+def bi_attention_ref(q, k, v_v, v_l, pad_v=None, pad_l=None):
+    """q [B,H,S,hd] (pre-scaled), k/v_l [B,H,T,hd], v_v [B,H,S,hd] ->
+    (out_v [B,H,S,hd], out_l [B,H,T,hd]).  Statement order follows
+    fuse_modules.py:174-217."""
+    b, h, s, hd = q.shape
+    t = k.shape[2]
+    qf, kf = q.reshape(b * h, s, hd), k.reshape(b * h, t, hd)
+    w = torch.bmm(qf, kf.transpose(1, 2))
+    w = w - w.max()
+    w = torch.clamp(w, min=-50000)
+    w = torch.clamp(w, max=50000)
+    wt = w.transpose(1, 2)
+    wl = wt - torch.max(wt, dim=-1, keepdim=True)[0]
+    wl = torch.clamp(wl, min=-50000)
+    wl = torch.clamp(wl, max=50000)
+    if pad_v is not None:
+        m = pad_v[:, None, None, :].repeat(1, h, 1, 1).flatten(0, 1)
+        wl = wl.masked_fill(m, float("-inf"))
+    wl = wl.softmax(dim=-1)
+    if pad_l is not None:
+        m = pad_l[:, None, None, :].repeat(1, h, 1, 1).flatten(0, 1)
+        w = w.masked_fill(m, float("-inf"))
+    wv = w.softmax(dim=-1)
+    out_v = torch.bmm(wv, v_l.reshape(b * h, t, hd)).view(b, h, s, hd)
+    out_l = torch.bmm(wl, v_v.reshape(b * h, s, hd)).view(b, h, t, hd)
+    return out_v, out_l
+
+
+def window_attention_ref(q, k, v, bias, mask, scale):
+    """q/k/v [B_, nH, N, hd]; bias [nH, N, N]; mask [nW, N, N] or None."""
+    attn = (q * scale) @ k.transpose(-2, -1)
+    attn = attn + bias.unsqueeze(0)
+    if mask is not None:
+        nw = mask.shape[0]
+        b_, nh, n, _ = attn.shape
+        attn = attn.view(b_ // nw, nw, nh, n, n) + mask.unsqueeze(1).unsqueeze(0)
+        attn = attn.view(-1, nh, n, n)
+    return torch.softmax(attn, dim=-1) @ v
+
+
+def attention_ref(q, k, v, mask=None, scale=None):
+    """q [B,H,Lq,hd], k/v [B,H,Lk,hd]; mask bool (True = attend) or additive."""
+    scale = q.shape[-1] ** -0.5 if scale is None else scale
+    s = (q @ k.transpose(-2, -1)) * scale
+    if mask is not None:
+        if mask.dtype == torch.bool:
+            s = s.masked_fill(~mask, float("-inf"))
+        else:
+            s = s + mask
+    return torch.softmax(s, dim=-1) @ v
+
+
+def contrastive_ref(x, text, text_token_mask, max_text_len=256):
+    res = x @ text.transpose(-1, -2)
+    res.masked_fill_(~text_token_mask[:, None, :], float("-inf"))
+    new = torch.full((*res.shape[:-1], max_text_len), float("-inf"), device=res.device)
+    new[..., : res.shape[-1]] = res
+    return new
+
+
+def phrase_masks_ref(input_ids, special_tokens):
+    """Loop over every special token in row-major order, previous column
+    carried across rows (bertwarper.py:240-262)."""
+    bs, n = input_ids.shape
+    special = torch.zeros((bs, n), dtype=torch.bool)
+    for tok in special_tokens:
+        special |= input_ids == tok
+    idxs = torch.nonzero(special)
+    mask = torch.eye(n, dtype=torch.bool).unsqueeze(0).repeat(bs, 1, 1)
+    pos = torch.zeros((bs, n), dtype=torch.long)
+    prev = 0
+    for i in range(idxs.shape[0]):
+        r, c = int(idxs[i, 0]), int(idxs[i, 1])
+        if c == 0 or c == n - 1:
+            mask[r, c, c] = True
+            pos[r, c] = 0
+        else:
+            mask[r, prev + 1:c + 1, prev + 1:c + 1] = True
+            pos[r, prev + 1:c + 1] = torch.arange(0, c - prev)
+        prev = c
+    return mask, pos

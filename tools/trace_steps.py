@@ -1,0 +1,69 @@
+"""Per-step kernel breakdown from a rocprofv3 kernel-trace CSV: steps are
+delimited by the fused AdamW kernel (one multi_tensor_apply chain per step);
+only steps after --skip optimizer steps are summarised."""
+import argparse
+import collections
+import csv
+import re
+
+
+def short(name):
+    n = re.sub(r"\(.*", "", name)
+    for key, lab in (("msda_fwd", "gd::msda_fwd"), ("msda_bwd", "gd::msda_bwd"), ("attn_fwd", "sdpa attn_fwd"),
+                     ("bwd_kernel_dq", "sdpa bwd_dq"), ("bwd_kernel_dk_dv", "sdpa bwd_dk_dv"),
+                     ("Cijk_", "hipBLASLt GEMM"), ("layer_norm", "layer_norm"), ("LayerNorm", "layer_norm"),
+                     ("GammaBeta", "layer_norm bwd"), ("ComputeGradInput", "layer_norm bwd"),
+                     ("conv", "conv"), ("reduce_kernel", "reduce"), ("softmax", "softmax"),
+                     ("FusedOpti", "adamw"), ("multi_tensor", "multi_tensor"), ("copy", "copy/cast"),
+                     ("elementwise", "elementwise"), ("index", "index/gather"), ("fill", "fill"),
+                     ("Fill", "fill"), ("scatter", "index/gather"), ("gather", "index/gather"),
+                     ("group_norm", "group_norm"), ("GroupNorm", "group_norm"), ("topk", "topk"),
+                     ("sort", "sort"), ("cat", "cat")):
+        if key in n:
+            return lab
+    return n[:60]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--skip", type=int, default=2)
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # step boundary = first fused AdamW kernel of a chain
+    bounds, last = [], -1
+    for i, r in enumerate(rows):
+        if "FusedOpti" in r["Kernel_Name"] or "fused_adam" in r["Kernel_Name"].lower():
+            if last < 0 or i - last > 50:
+                bounds.append(i)
+            last = i
+    if len(bounds) <= a.skip:
+        raise SystemExit(f"only {len(bounds)} optimizer steps found")
+    start = bounds[a.skip - 1] + 1 if a.skip > 0 else 0
+    sel = rows[start:]
+    nsteps = len(bounds) - a.skip
+    t_first = int(sel[0]["Start_Timestamp"])
+    t_last = int(sel[-1]["End_Timestamp"])
+    by = collections.defaultdict(lambda: [0, 0.0])
+    by_full = collections.defaultdict(lambda: [0, 0.0])
+    for r in sel:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        s = short(r["Kernel_Name"])
+        by[s][0] += 1
+        by[s][1] += d
+        by_full[r["Kernel_Name"][:100]][0] += 1
+        by_full[r["Kernel_Name"][:100]][1] += d
+    busy = sum(v[1] for v in by.values())
+    print(f"steps={nsteps} wall(first..last kernel)={((t_last - t_first) / 1e6) / nsteps:.1f} ms/step "
+          f"kernel-busy={busy / nsteps:.1f} ms/step kernels/step={len(sel) / nsteps:.0f}")
+    for k, (n, ms) in sorted(by.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        print(f"  {ms / nsteps:8.2f} ms/step {100 * ms / busy:5.1f}%  n/step={n / nsteps:7.1f}  {k}")
+    print("--- top individual kernels")
+    for k, (n, ms) in sorted(by_full.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        print(f"  {ms / nsteps:8.2f} ms/step  n/step={n / nsteps:6.1f} avg={ms / n * 1e3:8.1f}us  {k}")
+
+
+if __name__ == "__main__":
+    main()
