@@ -40,6 +40,7 @@
 #ifndef GDINO_AMD_H
 #define GDINO_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -104,6 +105,26 @@ gd_status gd_msda_backward(gd_dtype value_dtype, const void* value,
                            int num_levels, int num_query, int num_point,
                            void* grad_value, void* grad_sampling_loc,
                            void* grad_attn_weight, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* BiAttention bidirectional softmax (fuse_modules.py:174-217)               */
+/* ------------------------------------------------------------------------ */
+/*
+ * s        [B, H, S, T]  scores q.k^T (dtype F32 or BF16), T <= 1024
+ * pad_v    [B, S] uint8 (1 = padded image token) or NULL
+ * pad_l    [B, T] uint8 (1 = padded text token) or NULL
+ * pv       [B, H, S, T]  softmax over T (image -> text attention)
+ * pl       [B, H, S, T]  softmax over S, column-normalised (text -> image)
+ * workspace gd_biattn_workspace_bytes(B, H, S, T) bytes of device memory
+ */
+size_t gd_biattn_workspace_bytes(int B, int H, int S, int T);
+gd_status gd_biattn_softmax_fwd(gd_dtype dtype, const void* s, const uint8_t* pad_v,
+                                const uint8_t* pad_l, int B, int H, int S, int T, void* pv,
+                                void* pl, void* workspace, gd_stream_t stream);
+/* ds = pv * (dpv - rowsum(dpv * pv)) + pl * (dpl - colsum(dpl * pl)) */
+gd_status gd_biattn_softmax_bwd(gd_dtype dtype, const void* pv, const void* pl, const void* dpv,
+                                const void* dpl, int B, int H, int S, int T, void* ds,
+                                void* workspace, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

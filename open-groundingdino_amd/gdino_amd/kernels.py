@@ -129,3 +129,7 @@ def bi_attention(*args, **kw):
 
 def contrastive_logits(x, text, text_token_mask, max_text_len):
     return get("contrastive_logits")(x, text, text_token_mask, max_text_len)
+
+
+# HIP implementations register themselves as the defaults for CUDA tensors.
+from . import biattn  # noqa: E402,F401

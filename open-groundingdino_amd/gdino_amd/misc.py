@@ -11,6 +11,20 @@ import torch.distributed as dist
 from torch import Tensor, nn
 
 
+_CONSTS = {}
+
+
+def device_const(key, make, device) -> Tensor:
+    """A small constant tensor built on the host once per (key, device) and
+    kept resident (no host->device copy inside a captured HIP graph)."""
+    k = (key, str(device))
+    t = _CONSTS.get(k)
+    if t is None:
+        t = make().to(device)
+        _CONSTS[k] = t
+    return t
+
+
 class NestedTensor:
     """Batched images + padding mask (True on padded pixels).
     Contract of groundingdino/util/misc.py:399-480; the model also accepts any

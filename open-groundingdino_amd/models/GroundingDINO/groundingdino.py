@@ -137,47 +137,48 @@ class GroundingDINO(nn.Module):
         self.refpoint_embed = nn.Embedding(use_num_queries, self.query_dim)
 
     # ------------------------------------------------------------------ text
-    def encode_text(self, captions, device):
+    def prepare_text(self, captions, device):
+        """Host side of the text path: tokenize, phrase masks / position ids
+        (numpy, no device syncs), truncate to max_text_len, move once.
+        -> (dict of device tensors, tokenizer output for the loss)."""
         tokenized = self.tokenizer(captions, padding="longest", return_tensors="pt")
-        one_hot_token = tokenized
         self_masks, position_ids, _ = generate_masks_with_special_tokens_and_transfer_map(
             tokenized, self.specical_tokens, self.tokenizer)
-        tok = {k: v for k, v in tokenized.items()}
         n = self.max_text_len
+        tok = {k: v for k, v in tokenized.items()}
         if self_masks.shape[1] > n:
             self_masks = self_masks[:, :n, :n]
             position_ids = position_ids[:, :n]
             for k in ("input_ids", "attention_mask", "token_type_ids"):
                 tok[k] = tok[k][:, :n]
-        tok = {k: v.to(device, non_blocking=True) for k, v in tok.items()}
-        self_masks = self_masks.to(device, non_blocking=True)
-        position_ids = position_ids.to(device, non_blocking=True)
+        text = {"input_ids": tok["input_ids"], "token_type_ids": tok["token_type_ids"],
+                "text_token_mask": tok["attention_mask"].bool(), "self_masks": self_masks,
+                "position_ids": position_ids}
+        return {k: v.to(device, non_blocking=True) for k, v in text.items()}, tokenized
+
+    def encode_text(self, input_ids, token_type_ids, text_token_mask, self_masks, position_ids):
+        """BERT + feat_map -> text_dict (groundingdino.py:259-287)."""
         if self.sub_sentence_present:
-            enc_in = {k: v for k, v in tok.items() if k != "attention_mask"}
-            enc_in["attention_mask"] = self_masks
-            enc_in["position_ids"] = position_ids
+            bert_out = self.bert(input_ids=input_ids, token_type_ids=token_type_ids,
+                                 attention_mask=self_masks, position_ids=position_ids)
         else:
-            enc_in = tok
-        bert_out = self.bert(**enc_in)
+            bert_out = self.bert(input_ids=input_ids, token_type_ids=token_type_ids,
+                                 attention_mask=text_token_mask)
         encoded_text = self.feat_map(bert_out["last_hidden_state"])
-        text_token_mask = tok["attention_mask"].bool()
-        if encoded_text.shape[1] > n:
-            encoded_text = encoded_text[:, :n]
-            text_token_mask = text_token_mask[:, :n]
-            position_ids = position_ids[:, :n]
-            self_masks = self_masks[:, :n, :n]
-        text_dict = {"encoded_text": encoded_text, "text_token_mask": text_token_mask,
-                     "position_ids": position_ids, "text_self_attention_masks": self_masks}
-        return text_dict, one_hot_token
+        n = self.max_text_len
+        return {"encoded_text": encoded_text[:, :n], "text_token_mask": text_token_mask[:, :n],
+                "position_ids": position_ids[:, :n], "text_self_attention_masks": self_masks[:, :n, :n]}
 
     # --------------------------------------------------------------- forward
-    def forward(self, samples, targets: List = None, **kw):
-        captions = kw["captions"] if targets is None else [t["caption"] for t in targets]
-        if isinstance(samples, (list, torch.Tensor)):
-            samples = nested_tensor_from_tensor_list(samples)
-        device = samples.tensors.device
-        text_dict, one_hot_token = self.encode_text(captions, device)
-
+    def forward_core(self, images, image_mask, input_ids, token_type_ids, text_token_mask, self_masks,
+                     position_ids):
+        """Tensor-in / tensor-out body of the forward (no host syncs, static
+        shapes for a fixed batch geometry), the unit that gdino_amd.graphs
+        captures into one HIP graph for forward and one for backward.
+        -> (outputs_class [L,B,Q,256], outputs_coord [L,B,Q,4], text_mask [B,256],
+            interm_class, interm_coord, init_box_proposal)"""
+        text_dict = self.encode_text(input_ids, token_type_ids, text_token_mask, self_masks, position_ids)
+        samples = NestedTensor(images, image_mask)
         features, poss = self.backbone(samples)
         srcs, masks = [], []
         for lvl, feat in enumerate(features):
@@ -189,7 +190,7 @@ class GroundingDINO(nn.Module):
             n_back = len(srcs)
             for lvl in range(n_back, self.num_feature_levels):
                 src = self.input_proj[lvl](features[-1].tensors if lvl == n_back else srcs[-1])
-                mask = F.interpolate(samples.mask[None].float(), size=src.shape[-2:]).to(torch.bool)[0]
+                mask = F.interpolate(image_mask[None].float(), size=src.shape[-2:]).to(torch.bool)[0]
                 pos_l = self.backbone[1](NestedTensor(src, mask)).to(src.dtype)
                 srcs.append(src)
                 masks.append(mask)
@@ -203,18 +204,30 @@ class GroundingDINO(nn.Module):
             coords.append((box_embed(layer_hs) + inverse_sigmoid(ref_sig)).sigmoid())
         outputs_coord = torch.stack(coords)
         outputs_class = torch.stack([emb(layer_hs, text_dict) for emb, layer_hs in zip(self.class_embed, hs)])
-
-        out = {"pred_logits": outputs_class[-1], "pred_boxes": outputs_coord[-1]}
         bs, len_td = text_dict["text_token_mask"].shape
-        text_mask = torch.zeros(bs, self.max_text_len, dtype=torch.bool, device=device)
+        text_mask = torch.zeros(bs, self.max_text_len, dtype=torch.bool, device=images.device)
         text_mask[:, :len_td] = text_dict["text_token_mask"]
-        out["text_mask"] = text_mask
+        if hs_enc is not None:
+            interm_class = self.transformer.enc_out_class_embed(hs_enc[-1], text_dict)
+            return outputs_class, outputs_coord, text_mask, interm_class, ref_enc[-1], init_box_proposal
+        return outputs_class, outputs_coord, text_mask, None, None, None
+
+    def forward(self, samples, targets: List = None, **kw):
+        captions = kw["captions"] if targets is None else [t["caption"] for t in targets]
+        if isinstance(samples, (list, torch.Tensor)):
+            samples = nested_tensor_from_tensor_list(samples)
+        device = samples.tensors.device
+        text, one_hot_token = self.prepare_text(captions, device)
+        core = self._graphed_core if getattr(self, "_graphed_core", None) is not None else self.forward_core
+        (outputs_class, outputs_coord, text_mask, interm_class, interm_coord,
+         init_box_proposal) = core(samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
+                                   text["text_token_mask"], text["self_masks"], text["position_ids"])
+        out = {"pred_logits": outputs_class[-1], "pred_boxes": outputs_coord[-1], "text_mask": text_mask}
         if self.aux_loss:
             out["aux_outputs"] = self._set_aux_loss(outputs_class, outputs_coord)
         out["token"] = one_hot_token
-        if hs_enc is not None:
-            interm_class = self.transformer.enc_out_class_embed(hs_enc[-1], text_dict)
-            out["interm_outputs"] = {"pred_logits": interm_class, "pred_boxes": ref_enc[-1]}
+        if interm_class is not None:
+            out["interm_outputs"] = {"pred_logits": interm_class, "pred_boxes": interm_coord}
             out["interm_outputs_for_matching_pre"] = {"pred_logits": interm_class,
                                                       "pred_boxes": init_box_proposal}
         return out

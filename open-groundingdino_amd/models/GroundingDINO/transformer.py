@@ -22,7 +22,7 @@ import torch.utils.checkpoint as checkpoint
 from torch import Tensor, nn
 
 from gdino_amd.mha import MultiheadAttention
-from gdino_amd.misc import inverse_sigmoid
+from gdino_amd.misc import device_const, inverse_sigmoid
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
@@ -134,11 +134,13 @@ class Transformer(nn.Module):
         mask_flatten = torch.cat(flat_mask, 1)
         lvl_pos_embed_flatten = torch.cat(flat_pos, 1)
         device = src_flatten.device
-        spatial_shapes = torch.as_tensor(shapes_list, dtype=torch.long, device=device)
         starts = [0]
         for h, w in shapes_list[:-1]:
             starts.append(starts[-1] + h * w)
-        level_start_index = torch.as_tensor(starts, dtype=torch.long, device=device)
+        key = tuple(shapes_list)
+        spatial_shapes = device_const(("shapes",) + key,
+                                      lambda: torch.as_tensor(shapes_list, dtype=torch.long), device)
+        level_start_index = device_const(("lsi",) + key, lambda: torch.as_tensor(starts, dtype=torch.long), device)
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
 
         memory, memory_text = self.encoder(

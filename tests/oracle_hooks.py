@@ -14,10 +14,16 @@ class _OracleMSDA:
 
 @contextlib.contextmanager
 def oracle_msda():
+    """Route every HIP-only op to its oracle restatement (CPU tests)."""
     import models.GroundingDINO.ms_deform_attn as mod
+    from gdino_amd import kernels
+    from oracle.blocks import bi_attention_ref
+
     prev = mod.MSDeformAttnFunction
     mod.MSDeformAttnFunction = _OracleMSDA
     try:
-        yield
+        with kernels.override("bi_attention", lambda q, k, vv, vl, pv=None, pl=None, p=0.0:
+                              bi_attention_ref(q, k, vv, vl, pv, pl)):
+            yield
     finally:
         mod.MSDeformAttnFunction = prev

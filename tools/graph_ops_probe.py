@@ -1,0 +1,114 @@
+"""Which op breaks hipGraph instantiation?  One make_graphed_callables per
+subprocess over a tiny module."""
+import faulthandler
+import os
+import subprocess
+import sys
+
+faulthandler.enable()
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
+
+CASES = ["msda_mod_bf16_eagerfirst", "full_model"]
+
+
+def run(case):
+    import torch
+    from torch import nn
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    eager_first = case.endswith("_eagerfirst")
+    case = case.replace("_eagerfirst", "")
+    amp = case.endswith("bf16")
+    if case == "full_model":
+        return run_full()
+    shapes = torch.as_tensor([(32, 40), (16, 20), (8, 10), (4, 5)], device=dev)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S = int(shapes.prod(1).sum())
+    if case.startswith("linear"):
+        mod = nn.Linear(256, 256).to(dev)
+        args = (torch.randn(2, S, 256, device=dev, requires_grad=True),)
+    elif case.startswith("softmax"):
+        class M(nn.Module):
+            def __init__(s):
+                super().__init__()
+                s.l = nn.Linear(256, 128).to(dev)
+
+            def forward(s, x):
+                return s.l(x).view(2, S, 8, 16).softmax(-1)
+        mod = M()
+        args = (torch.randn(2, S, 256, device=dev, requires_grad=True),)
+    elif case.startswith("msda_fn"):
+        from models.GroundingDINO.ops.functions.ms_deform_attn_func import MSDeformAttnFunction
+
+        class M(nn.Module):
+            def forward(s, v, loc, a):
+                return MSDeformAttnFunction.apply(v.to(torch.bfloat16), shapes, lsi, loc, a, 64)
+        mod = M()
+        args = (torch.randn(2, S, 8, 32, device=dev, requires_grad=True),
+                torch.rand(2, S, 8, 4, 4, 2, device=dev, requires_grad=True),
+                torch.rand(2, S, 8, 4, 4, device=dev, requires_grad=True))
+    else:
+        from models.GroundingDINO.ms_deform_attn import MultiScaleDeformableAttention
+        m = MultiScaleDeformableAttention(256, 8, 4, 4, batch_first=True, dropout=0.0).to(dev)
+
+        class M(nn.Module):
+            def __init__(s):
+                super().__init__()
+                s.m = m
+
+            def forward(s, x, ref):
+                return s.m(query=x, value=x, reference_points=ref, spatial_shapes=shapes, level_start_index=lsi)
+        mod = M()
+        args = (torch.randn(2, S, 256, device=dev, requires_grad=True), torch.rand(2, S, 4, 2, device=dev))
+    if eager_first:
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
+            o = mod(*args)
+        o.float().sum().backward()
+        del o
+        for p in mod.parameters():
+            p.grad = None
+        torch.cuda.synchronize()
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
+        g = torch.cuda.make_graphed_callables(mod, args, num_warmup_iters=2)
+    out = g(*args)
+    out.float().sum().backward()
+    torch.cuda.synchronize()
+    print(case, "ok", flush=True)
+
+
+def run_full():
+    import torch
+    from gdino_amd import graphs
+    from gdino_amd.config import make_args
+    from gdino_amd.train import build_training, synthetic_batch
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    model, crit, _, opt = build_training(make_args(device="cuda"), dev)
+    model.train()
+    samples, targets, caps, cats = synthetic_batch(2, 512, 640, n_boxes=8, n_tokens=256, seed=1, device=dev)
+    text, _ = model.prepare_text(caps, dev)
+    ins = (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"], text["text_token_mask"],
+           text["self_masks"], text["position_ids"])
+    graphs.capture(model, ins)
+    torch.cuda.synchronize()
+    print("full: captured", flush=True)
+    outs = model._graphed_core(*ins)
+    torch.cuda.synchronize()
+    print("full: fwd replay ok", [tuple(o.shape) for o in outs if o is not None], flush=True)
+    loss = sum(o.float().mean() for o in outs if o is not None and o.is_floating_point() and o.requires_grad)
+    loss.backward()
+    torch.cuda.synchronize()
+    print("full: bwd replay ok", flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        run(sys.argv[1])
+        sys.exit(0)
+    for c in CASES:
+        r = subprocess.run([sys.executable, "-X", "faulthandler", __file__, c], timeout=200,
+                           capture_output=True, text=True)
+        tail = "\n".join([ln for ln in (r.stdout + r.stderr).splitlines() if "Warning" not in ln
+                          and "amdgpu.ids" not in ln and "run_backward" not in ln][-6:])
+        print(f"== {c}: rc={r.returncode}\n{tail}", flush=True)
