@@ -55,11 +55,10 @@ def parse():
 def setup_dist(n):
     if n <= 1 and "RANK" not in os.environ:
         return 0, 1, 0
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    torch.cuda.set_device(local)  # bind the device before RCCL creates its communicator
     dist.init_process_group("nccl")
-    rank, world = dist.get_rank(), dist.get_world_size()
-    local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    return rank, world, local
+    return dist.get_rank(), dist.get_world_size(), local
 
 
 def cpu_baseline(bs):
@@ -128,9 +127,11 @@ def main():
     model, criterion, _, optimizer = build_training(args, device)
     model.train()
     if world > 1:
+        # reference main.py:258-261 (DDP + static graph); buckets sized for
+        # xGMI rings (fewer, larger all-reduces), launched as backward
+        # produces them so RCCL overlaps the rest of the backward pass
         model = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local], bucket_cap_mb=a.bucket_mb, gradient_as_bucket_view=True,
-            static_graph=True)
+            model, device_ids=[local], bucket_cap_mb=a.bucket_mb, static_graph=True)
     samples, targets, captions, cats = synthetic_batch(a.bs, a.height, a.width, n_boxes=8, n_tokens=256,
                                                        seed=1000 + rank, device=device)
 

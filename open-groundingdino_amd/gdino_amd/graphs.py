@@ -18,6 +18,7 @@ iterations do it), and the HIP kernels launched on the current stream.
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence
 
 import torch
@@ -51,8 +52,17 @@ def capture(model, sample_inputs: Sequence[torch.Tensor], amp_dtype=torch.bfloat
         graphed = torch.cuda.make_graphed_callables(core, tuple(sample_inputs), num_warmup_iters=warmup)
     none_mask = core._none_mask
 
+    debug = os.environ.get("GDINO_GRAPH_DEBUG") == "1"
+
     def call(*args):
-        outs = iter(graphed(*args))
+        if debug:
+            torch.cuda.synchronize()
+            print("graphs: pre-replay sync ok", flush=True)
+        res = graphed(*args)
+        if debug:
+            torch.cuda.synchronize()
+            print("graphs: replay sync ok", flush=True)
+        outs = iter(res)
         return tuple(None if is_none else next(outs) for is_none in none_mask)
 
     model._graphed_core = call

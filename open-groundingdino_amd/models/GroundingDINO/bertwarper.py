@@ -120,8 +120,8 @@ def _phrase_blocks(ids: np.ndarray, special_ids) -> tuple:
 def generate_masks_with_special_tokens(tokenized, special_tokens_list, tokenizer):
     ids = tokenized["input_ids"]
     mask, pos, _ = _phrase_blocks(ids.cpu().numpy(), special_tokens_list)
-    return (torch.from_numpy(mask).to(ids.device, non_blocking=True),
-            torch.from_numpy(pos).to(ids.device, non_blocking=True))
+    return (torch.from_numpy(mask).to(ids.device),
+            torch.from_numpy(pos).to(ids.device))
 
 
 def generate_masks_with_special_tokens_and_transfer_map(tokenized, special_tokens_list, tokenizer):
@@ -131,5 +131,5 @@ def generate_masks_with_special_tokens_and_transfer_map(tokenized, special_token
     cate_t: List[torch.Tensor] = [
         torch.from_numpy(np.stack(c)).to(dev) if c else torch.zeros((0, ids.shape[1]), dtype=torch.bool, device=dev)
         for c in cate]
-    return (torch.from_numpy(mask).to(dev, non_blocking=True),
-            torch.from_numpy(pos).to(dev, non_blocking=True), cate_t)
+    return (torch.from_numpy(mask).to(dev),
+            torch.from_numpy(pos).to(dev), cate_t)

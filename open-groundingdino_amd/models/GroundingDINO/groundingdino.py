@@ -154,7 +154,7 @@ class GroundingDINO(nn.Module):
         text = {"input_ids": tok["input_ids"], "token_type_ids": tok["token_type_ids"],
                 "text_token_mask": tok["attention_mask"].bool(), "self_masks": self_masks,
                 "position_ids": position_ids}
-        return {k: v.to(device, non_blocking=True) for k, v in text.items()}, tokenized
+        return {k: v.to(device) for k, v in text.items()}, tokenized
 
     def encode_text(self, input_ids, token_type_ids, text_token_mask, self_masks, position_ids):
         """BERT + feat_map -> text_dict (groundingdino.py:259-287)."""

@@ -9,7 +9,7 @@ faulthandler.enable()
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
-CASES = ["msda_mod_bf16_eagerfirst", "full_model"]
+CASES = ["full_model"]
 
 
 def run(case):
@@ -86,7 +86,8 @@ def run_full():
     torch.manual_seed(0)
     model, crit, _, opt = build_training(make_args(device="cuda"), dev)
     model.train()
-    samples, targets, caps, cats = synthetic_batch(2, 512, 640, n_boxes=8, n_tokens=256, seed=1, device=dev)
+    H, W = (int(v) for v in os.environ.get("GP_HW", "512x640").split("x"))
+    samples, targets, caps, cats = synthetic_batch(2, H, W, n_boxes=8, n_tokens=256, seed=1, device=dev)
     text, _ = model.prepare_text(caps, dev)
     ins = (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"], text["text_token_mask"],
            text["self_masks"], text["position_ids"])
