@@ -62,11 +62,18 @@ def init_msda_parameters(mod: nn.Module, num_heads: int, num_levels: int, num_po
     constant_(mod.output_proj.bias.data, 0.0)
 
 
+def _loc_dtype(t: torch.Tensor) -> torch.dtype:
+    """Sampling locations / weights are computed in fp32 (fp64 for fp64
+    models), whatever the autocast dtype of the projections."""
+    return torch.float64 if t.dtype == torch.float64 else torch.float32
+
+
 def sampling_locations_from(reference_points, sampling_offsets, spatial_shapes, num_points):
     """Reference points + learned offsets -> normalized sampling locations
-    [N, Lq, M, L, P, 2] in fp32 (ms_deform_attn.py:310-329)."""
-    off = sampling_offsets.float()
-    ref = reference_points.float()
+    [N, Lq, M, L, P, 2] in fp32 / fp64 (ms_deform_attn.py:310-329)."""
+    ct = torch.promote_types(_loc_dtype(sampling_offsets), _loc_dtype(reference_points))
+    off = sampling_offsets.to(ct)
+    ref = reference_points.to(ct)
     if ref.shape[-1] == 2:
         normalizer = torch.stack([spatial_shapes[..., 1], spatial_shapes[..., 0]], -1).to(off.dtype)
         return ref[:, :, None, :, None, :] + off / normalizer[None, None, None, :, None, :]
@@ -88,7 +95,7 @@ def msda_attend(mod, query, value, reference_points, spatial_shapes, level_start
     value = value.view(bs, num_value, num_heads, -1)
     offsets = mod.sampling_offsets(query).view(bs, num_query, num_heads, num_levels, num_points, 2)
     attn = mod.attention_weights(query).view(bs, num_query, num_heads, num_levels * num_points)
-    attn = attn.float().softmax(-1).view(bs, num_query, num_heads, num_levels, num_points)
+    attn = attn.to(_loc_dtype(attn)).softmax(-1).view(bs, num_query, num_heads, num_levels, num_points)
     loc = sampling_locations_from(reference_points, offsets, spatial_shapes, num_points)
     if value.dtype == torch.float16:  # kernels run fp32 / bf16 / fp64 value
         value = value.float()

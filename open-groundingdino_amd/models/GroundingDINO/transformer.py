@@ -402,7 +402,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
     def forward_ffn(self, tgt):
         # the reference runs the decoder FFN outside autocast (fp32, :870-875)
         with torch.autocast(device_type=tgt.device.type, enabled=False):
-            t = tgt.float()
+            t = tgt.float() if tgt.dtype in (torch.float16, torch.bfloat16) else tgt
             tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(t))))
         return self.norm3(tgt + self.dropout4(tgt2))
 

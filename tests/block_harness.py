@@ -1,0 +1,179 @@
+"""Runs the PRODUCT modules on the block-golden cases (tests/golden/
+block_spec.py) and compares with the reference-generated fixtures
+(tests/golden/make_block_golden.py).  Shared by the CPU tests (fp64, HIP-only
+ops routed to the oracle) and the GPU tests (fp32 on the HIP path)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+from conftest import GOLDEN
+
+sys.path.insert(0, GOLDEN)
+import block_spec as spec  # noqa: E402
+
+
+def fixture(name):
+    z = np.load(os.path.join(GOLDEN, f"block_{name}.npz"))
+    data = {k: z[k] for k in z.files if k != "meta_json"}
+    return data, json.loads(str(z["meta_json"]))
+
+
+def rel_err(mine, ref):
+    mine = torch.as_tensor(np.asarray(mine) if not torch.is_tensor(mine) else mine.detach().cpu()).double()
+    ref = torch.as_tensor(ref).double()
+    assert mine.shape == ref.shape, (tuple(mine.shape), tuple(ref.shape))
+    finite = torch.isfinite(ref)
+    assert torch.equal(finite, torch.isfinite(mine)), "non-finite pattern differs"
+    if not finite.any():
+        return 0.0
+    return float((mine[finite] - ref[finite]).abs().max() / ref[finite].abs().max().clamp_min(1e-30))
+
+
+def _store_pgrad(res, name, grad):
+    g = grad.detach().double().cpu()
+    res["pgrad." + name] = g.flatten()[:4096].numpy()
+    res["pgradsum." + name] = np.array([float(g.sum()), float(g.abs().sum())])
+
+
+def _move(x, device, dtype):
+    return x.to(device, dtype) if x.is_floating_point() else x.to(device)
+
+
+def run_biattn(device="cpu", dtype=torch.float64):
+    from models.GroundingDINO.fuse_modules import BiAttentionBlock
+    m = BiAttentionBlock(**spec.BIATTN, dropout=0.0, drop_path=0.0)
+    ck = spec.fill_params(m.to(dtype))
+    m = m.to(device).eval()
+    inp = {k: _move(v, device, dtype) for k, v in spec.biattn_inputs().items()}
+    v = inp["v"].clone().requires_grad_(True)
+    l = inp["l"].clone().requires_grad_(True)
+    ov, ol = m(v, l, attention_mask_v=inp["mask_v"], attention_mask_l=inp["mask_l"])
+    ((ov * inp["gv"]).sum() + (ol * inp["gl"]).sum()).backward()
+    res = {"out_v": ov, "out_l": ol, "grad_v": v.grad, "grad_l": l.grad}
+    for name, p in m.named_parameters():
+        _store_pgrad(res, name, p.grad)
+    return res, {"weights_checksum": ck}
+
+
+def run_swin(device="cpu", dtype=torch.float64):
+    from gdino_amd.misc import NestedTensor
+    from models.GroundingDINO.backbone.swin_transformer import SwinTransformer
+    m = SwinTransformer(**spec.SWIN)
+    ck = spec.fill_params(m.to(dtype))
+    m = m.to(device).eval()
+    inp = spec.swin_inputs()
+    x = inp["x"].to(device, dtype).requires_grad_(True)
+    outs = m(NestedTensor(x, inp["mask"].to(device)))
+    res, loss = {}, 0.0
+    for k, nt in outs.items():
+        res[f"feat{k}"] = nt.tensors
+        res[f"mask{k}"] = nt.mask
+        g = spec.rand(nt.tensors.shape, f"swin_g{k}").to(device, dtype)
+        loss = loss + (nt.tensors * g).sum()
+    loss.backward()
+    res["grad_x"] = x.grad
+    named = dict(m.named_parameters())
+    for name in ("patch_embed.proj.weight", "layers.0.blocks.1.attn.relative_position_bias_table",
+                 "layers.2.blocks.0.attn.qkv.weight", "layers.3.blocks.1.mlp.fc2.weight", "norm3.weight"):
+        _store_pgrad(res, name, named[name].grad)
+    return res, {"weights_checksum": ck, "keys": sorted(outs.keys())}
+
+
+def run_pos(device="cpu", dtype=torch.float64):
+    from gdino_amd.misc import NestedTensor
+    from models.GroundingDINO.backbone.position_encoding import PositionEmbeddingSineHW
+    inp = spec.swin_inputs()
+    pe = PositionEmbeddingSineHW(num_pos_feats=64, temperatureH=20, temperatureW=20, normalize=True)
+    return {"pos": pe(NestedTensor(inp["x"].to(device, dtype), inp["mask"].to(device)))}, {}
+
+
+def run_contrastive(device="cpu", dtype=torch.float64):
+    from models.GroundingDINO.utils import ContrastiveEmbed
+    x = spec.rand((2, 30, 64), "ce_x").to(device, dtype)
+    text = spec.rand((2, spec.TEXT_LEN, 64), "ce_text").to(device, dtype)
+    token_mask, _, _ = spec.phrase_text()
+    out = ContrastiveEmbed()(x, {"encoded_text": text, "text_token_mask": token_mask.to(device)})
+    return {"logits": out}, {}
+
+
+def run_proposals(device="cpu", dtype=torch.float64, fix=None):
+    from models.GroundingDINO.utils import gen_encoder_output_proposals
+    shapes = torch.as_tensor(spec.LEVELS, dtype=torch.long)
+    memory = torch.as_tensor(fix["memory"]).to(device, dtype)
+    mask = torch.as_tensor(fix["mask"]).to(device)
+    om, op = gen_encoder_output_proposals(memory, mask, shapes.to(device))
+    return {"output_memory": om, "output_proposals": op}, {}
+
+
+def run_transformer(device="cpu", dtype=torch.float64):
+    from models.GroundingDINO.transformer import Transformer
+    from models.GroundingDINO.utils import MLP, ContrastiveEmbed
+    torch.manual_seed(0)
+    t = Transformer(**spec.TRANSFORMER)
+    spec.wire_heads(t, MLP, ContrastiveEmbed)
+    ck = spec.fill_params(t.to(dtype))
+    t = t.to(device).eval()
+    inp = spec.transformer_inputs()
+    srcs = [s.to(device, dtype).requires_grad_(True) for s in inp["srcs"]]
+    text = inp["text"].to(device, dtype).requires_grad_(True)
+    td = spec.transformer_text_dict(inp, dtype, device)
+    td["encoded_text"] = text
+    masks = [m.to(device) for m in inp["masks"]]
+    poss = [p.to(device, dtype) for p in inp["poss"]]
+    hs, refs, hs_enc, ref_enc, init_box = t(srcs, masks, None, poss, None, None, td)
+    loss = (torch.stack(hs) * inp["g_hs"].to(device, dtype)).sum() \
+        + (torch.stack(refs) * inp["g_ref"].to(device, dtype)).sum() \
+        + (hs_enc * inp["g_enc"].to(device, dtype)).sum()
+    loss.backward()
+    res = {f"hs{i}": h for i, h in enumerate(hs)}
+    res.update({f"ref{i}": r for i, r in enumerate(refs)})
+    res.update(hs_enc=hs_enc, ref_enc=ref_enc, init_box_proposal=init_box, grad_text=text.grad)
+    res.update({f"grad_src{i}": s.grad for i, s in enumerate(srcs)})
+    named = dict(t.named_parameters())
+    for name in ("level_embed", "encoder.layers.0.self_attn.sampling_offsets.weight",
+                 "encoder.fusion_layers.1.attn.values_l_proj.weight", "encoder.text_layers.0.self_attn.in_proj_weight",
+                 "decoder.layers.1.cross_attn.value_proj.weight", "decoder.layers.0.ca_text.in_proj_weight",
+                 "decoder.bbox_embed.0.layers.2.weight", "enc_output.weight", "tgt_embed.weight"):
+        if name in named and named[name].grad is not None:
+            _store_pgrad(res, name, named[name].grad)
+    return res, {"weights_checksum": ck, "param_names": sorted(named.keys())}
+
+
+RUNNERS = {"biattn": run_biattn, "swin": run_swin, "pos": run_pos, "contrastive": run_contrastive,
+           "proposals": run_proposals, "transformer": run_transformer}
+
+
+def compare(name, device="cpu", dtype=torch.float64, tol=1e-9, grad_tol=None, skip=()):
+    """Run case `name` on the product and compare every fixture array.
+    Returns {key: relative error}.  Parameter-gradient samples were stored in
+    fp32, so they are held to max(tol, 1e-6)."""
+    fix, meta = fixture(name)
+    runner = RUNNERS[name]
+    res, my_meta = runner(device, dtype, fix) if name == "proposals" else runner(device, dtype)
+    if "weights_checksum" in meta:
+        assert abs(my_meta["weights_checksum"] - meta["weights_checksum"]) <= 1e-9 * meta["weights_checksum"], \
+            "parameter names/shapes differ from the reference"
+    if "param_names" in meta:
+        assert my_meta["param_names"] == meta["param_names"]
+    errs = {}
+    grad_tol = tol if grad_tol is None else grad_tol
+    for key, ref in fix.items():
+        if key in ("memory", "mask") or key in skip:
+            continue
+        assert key in res, f"{name}: product produced no '{key}'"
+        mine = res[key]
+        if key.startswith("mask"):
+            assert np.array_equal(np.asarray(mine.cpu()), ref), key
+            continue
+        e = rel_err(mine, ref)
+        errs[key] = e
+        lim = grad_tol if ("grad" in key) else tol
+        if key.startswith("pgrad.") or ref.dtype == np.float32:
+            lim = max(lim, 1e-6)  # stored (or produced by the reference) in fp32
+        assert e <= lim, f"{name}.{key}: rel err {e:.3e} > {lim:.1e}"
+    return errs

@@ -1,0 +1,140 @@
+"""Shared specification of the block-level golden cases (TEST INFRASTRUCTURE).
+
+Used by tests/golden/make_block_golden.py (which runs the REFERENCE modules
+in this container to produce the fixtures) and by the tests (which run the
+product modules on the same inputs).  Weights are not stored in the fixtures:
+both sides fill every parameter deterministically from its state-dict name
+(`fill_params`), so the fixture only carries inputs, outputs, gradients and a
+checksum of the weights.  Same names + same shapes => same weights, which is
+also the state-dict compatibility check.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+
+import torch
+
+SEED = 20240917
+
+# Small but structurally complete configurations.  MSDA keeps M*D with D=32,
+# L=P=4 so that the GPU runs the vectorised kernels, not only the generic ones.
+BIATTN = dict(v_dim=64, l_dim=48, embed_dim=128, num_heads=4)
+SWIN = dict(pretrain_img_size=224, embed_dim=32, depths=[2, 2, 2, 2], num_heads=[1, 2, 4, 8], window_size=7,
+            out_indices=(1, 2, 3), drop_path_rate=0.0)
+TRANSFORMER = dict(d_model=256, nhead=8, num_queries=30, num_encoder_layers=2, num_decoder_layers=2,
+                   dim_feedforward=256, dropout=0.0, activation="relu", normalize_before=False,
+                   return_intermediate_dec=True, query_dim=4, num_patterns=0, num_feature_levels=4,
+                   enc_n_points=4, dec_n_points=4, learnable_tgt_init=True, two_stage_type="standard",
+                   embed_init_tgt=True, use_text_enhancer=True, use_fusion_layer=True, use_checkpoint=False,
+                   use_transformer_ckpt=False, use_text_cross_attention=True, text_dropout=0.0,
+                   fusion_dropout=0.0, fusion_droppath=0.0)
+LEVELS = [(6, 8), (3, 4), (2, 2), (1, 1)]
+TEXT_LEN = 13
+
+
+def _gen(name: str, salt: int = 0) -> torch.Generator:
+    return torch.Generator().manual_seed((zlib.crc32(name.encode()) ^ SEED ^ salt) & 0x7FFFFFFF)
+
+
+def fill_params(module: torch.nn.Module, salt: int = 0) -> float:
+    """Deterministic, name-keyed parameter values (fp64).  Matrices get
+    N(0, 1/fan_in); 1-D 'weight'/'gamma' vectors 1 + N(0, 0.1^2) (LayerNorm
+    scales, layer-scale gammas); other 1-D vectors N(0, 0.1^2).  Returns a
+    checksum (sum of |p|) for the fixture."""
+    total = 0.0
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            g = _gen(name, salt)
+            if p.dim() >= 2:
+                fan_in = math.prod(p.shape[1:])
+                v = torch.randn(p.shape, generator=g, dtype=torch.float64) / math.sqrt(fan_in)
+            elif name.endswith("weight") or "gamma" in name:
+                v = 1.0 + 0.1 * torch.randn(p.shape, generator=g, dtype=torch.float64)
+            else:
+                v = 0.1 * torch.randn(p.shape, generator=g, dtype=torch.float64)
+            p.copy_(v.to(p.dtype))
+            total += float(v.abs().sum())
+    return total
+
+
+def rand(shape, name, scale=1.0):
+    return torch.randn(shape, generator=_gen("input:" + name), dtype=torch.float64) * scale
+
+
+def biattn_inputs():
+    v = rand((2, 50, BIATTN["v_dim"]), "v")
+    l = rand((2, TEXT_LEN, BIATTN["l_dim"]), "l")
+    mask_v = torch.zeros(2, 50, dtype=torch.bool)
+    mask_v[1, 40:] = True
+    mask_l = torch.zeros(2, TEXT_LEN, dtype=torch.bool)
+    mask_l[0, 9:] = True
+    gv = rand((2, 50, BIATTN["v_dim"]), "gv")
+    gl = rand((2, TEXT_LEN, BIATTN["l_dim"]), "gl")
+    return dict(v=v, l=l, mask_v=mask_v, mask_l=mask_l, gv=gv, gl=gl)
+
+
+def swin_inputs():
+    x = rand((2, 3, 96, 128), "img")
+    mask = torch.zeros(2, 96, 128, dtype=torch.bool)
+    mask[1, :, 96:] = True  # second image padded on the right
+    mask[1, 80:, :] = True
+    x = x.masked_fill(mask[:, None], 0.0)
+    return dict(x=x, mask=mask)
+
+
+def phrase_text(bs=2, t=TEXT_LEN):
+    """Token-level inputs as BertModelWarper / the model produce them:
+    valid-token mask, per-phrase position ids, block-diagonal phrase
+    self-attention masks (sample 0 has 3 phrases and 4 pad tokens, sample 1
+    two phrases and no padding)."""
+    token_mask = torch.ones(bs, t, dtype=torch.bool)
+    token_mask[0, 9:] = False
+    blocks = [[(0, 1), (1, 4), (4, 7), (7, 8), (8, 9)] + [(i, i + 1) for i in range(9, t)],
+              [(0, 1), (1, 6), (6, 12), (12, 13)]]
+    sa = torch.zeros(bs, t, t, dtype=torch.bool)
+    pos = torch.zeros(bs, t, dtype=torch.long)
+    for b, bl in enumerate(blocks):
+        for s, e in bl:
+            sa[b, s:e, s:e] = True
+            pos[b, s:e] = torch.arange(e - s)
+    return token_mask, pos, sa
+
+
+def transformer_inputs():
+    d = TRANSFORMER["d_model"]
+    srcs, masks, poss = [], [], []
+    for i, (h, w) in enumerate(LEVELS):
+        srcs.append(rand((2, d, h, w), f"src{i}"))
+        m = torch.zeros(2, h, w, dtype=torch.bool)
+        if w > 1:
+            m[1, :, w - max(1, w // 4):] = True
+        masks.append(m)
+        poss.append(rand((2, d, h, w), f"pos{i}", 0.5))
+    token_mask, pos_ids, sa = phrase_text()
+    text = rand((2, TEXT_LEN, d), "text")
+    g_hs = rand((TRANSFORMER["num_decoder_layers"], 2, TRANSFORMER["num_queries"], d), "g_hs")
+    g_ref = rand((TRANSFORMER["num_decoder_layers"] + 1, 2, TRANSFORMER["num_queries"], 4), "g_ref")
+    g_enc = rand((1, 2, TRANSFORMER["num_queries"], d), "g_enc")
+    return dict(srcs=srcs, masks=masks, poss=poss, text=text, token_mask=token_mask, pos_ids=pos_ids,
+                text_sa=sa, g_hs=g_hs, g_ref=g_ref, g_enc=g_enc)
+
+
+def wire_heads(transformer, mlp_cls, contrastive_cls):
+    """GroundingDINO.__init__'s head wiring (groundingdino.py:165-201) with
+    cfg_odvg's sharing flags: decoder bbox MLP shared over layers, separate
+    two-stage bbox MLP, parameter-free contrastive heads."""
+    d = transformer.d_model
+    n = transformer.num_decoder_layers
+    bbox = mlp_cls(d, d, 4, 3)
+    ce = contrastive_cls()
+    transformer.decoder.bbox_embed = torch.nn.ModuleList([bbox for _ in range(n)])
+    transformer.decoder.class_embed = torch.nn.ModuleList([ce for _ in range(n)])
+    transformer.enc_out_bbox_embed = mlp_cls(d, d, 4, 3)
+    transformer.enc_out_class_embed = contrastive_cls()
+    return transformer
+
+
+def transformer_text_dict(inp, dtype=torch.float64, device="cpu"):
+    return {"encoded_text": inp["text"].to(device, dtype), "text_token_mask": inp["token_mask"].to(device),
+            "position_ids": inp["pos_ids"].to(device), "text_self_attention_masks": inp["text_sa"].to(device)}

@@ -8,7 +8,7 @@ import re
 
 
 def short(name):
-    n = re.sub(r"\(.*", "", name)
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))
     for key, lab in (("msda_fwd", "gd::msda_fwd"), ("msda_bwd", "gd::msda_bwd"), ("attn_fwd", "sdpa attn_fwd"),
                      ("bwd_kernel_dq", "sdpa bwd_dq"), ("bwd_kernel_dk_dv", "sdpa bwd_dk_dv"),
                      ("Cijk_", "hipBLASLt GEMM"), ("layer_norm", "layer_norm"), ("LayerNorm", "layer_norm"),
@@ -36,7 +36,7 @@ def main():
     bounds, last = [], -1
     for i, r in enumerate(rows):
         if "FusedOpti" in r["Kernel_Name"] or "fused_adam" in r["Kernel_Name"].lower():
-            if last < 0 or i - last > 50:
+            if last < 0 or i - last > 1000:  # one chain per step (param groups launch separately)
                 bounds.append(i)
             last = i
     if len(bounds) <= a.skip:
@@ -44,6 +44,7 @@ def main():
     start = bounds[a.skip - 1] + 1 if a.skip > 0 else 0
     sel = rows[start:]
     nsteps = len(bounds) - a.skip
+    print(f"# optimizer chains found at kernel indices {bounds}")
     t_first = int(sel[0]["Start_Timestamp"])
     t_last = int(sel[-1]["End_Timestamp"])
     by = collections.defaultdict(lambda: [0, 0.0])
@@ -60,6 +61,19 @@ def main():
           f"kernel-busy={busy / nsteps:.1f} ms/step kernels/step={len(sel) / nsteps:.0f}")
     for k, (n, ms) in sorted(by.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"  {ms / nsteps:8.2f} ms/step {100 * ms / busy:5.1f}%  n/step={n / nsteps:7.1f}  {k}")
+    print("--- gd:: kernels by launch grid (steady-state steps)")
+    gd = collections.defaultdict(lambda: [0, 0.0])
+    for r in sel:
+        if "gd::" not in r["Kernel_Name"]:
+            continue
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        key = (re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).replace("void ", ""),
+               int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]))
+        gd[key][0] += 1
+        gd[key][1] += d
+    for (k, gx, gy), (n, us) in sorted(gd.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {k:45s} grid=({gx},{gy}) launches/step={n / nsteps:5.1f} avg={us / n:9.1f}us "
+              f"total={us / nsteps / 1e3:7.2f} ms/step")
     print("--- top individual kernels")
     for k, (n, ms) in sorted(by_full.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"  {ms / nsteps:8.2f} ms/step  n/step={n / nsteps:6.1f} avg={ms / n * 1e3:8.1f}us  {k}")
