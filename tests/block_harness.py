@@ -144,8 +144,28 @@ def run_transformer(device="cpu", dtype=torch.float64):
     return res, {"weights_checksum": ck, "param_names": sorted(named.keys())}
 
 
+def run_criterion(device="cpu", dtype=torch.float32):
+    from gdino_amd.tokenizer import OfflineBertTokenizer
+    from models.GroundingDINO.groundingdino import SetCriterion
+    from models.GroundingDINO.matcher import HungarianMatcher
+    inp = spec.criterion_inputs(OfflineBertTokenizer())
+    inp["targets"] = [{k: v.to(device) for k, v in t.items()} for t in inp["targets"]]
+    crit = SetCriterion(HungarianMatcher(**spec.MATCHER), spec.criterion_weight_dict(), spec.FOCAL_ALPHA,
+                        spec.FOCAL_GAMMA, ["labels", "boxes"])
+    outputs, leaves = spec.criterion_outputs(inp, device, dtype)
+    losses = crit(outputs, inp["targets"], inp["cat_list"], inp["captions"])
+    wd = crit.weight_dict
+    total = sum(losses[k] * wd[k] for k in losses if k in wd)
+    total.backward()
+    res = {"loss." + k: v.detach() for k, v in losses.items()}
+    res["total"] = total.detach()
+    res.update({"grad." + k: v.grad for k, v in leaves.items()})
+    return res, {"loss_keys": sorted(losses.keys())}
+
+
 RUNNERS = {"biattn": run_biattn, "swin": run_swin, "pos": run_pos, "contrastive": run_contrastive,
-           "proposals": run_proposals, "transformer": run_transformer}
+           "proposals": run_proposals, "transformer": run_transformer,
+           "criterion": run_criterion}
 
 
 def compare(name, device="cpu", dtype=torch.float64, tol=1e-9, grad_tol=None, skip=()):
@@ -160,6 +180,8 @@ def compare(name, device="cpu", dtype=torch.float64, tol=1e-9, grad_tol=None, sk
             "parameter names/shapes differ from the reference"
     if "param_names" in meta:
         assert my_meta["param_names"] == meta["param_names"]
+    if "loss_keys" in meta:
+        assert my_meta["loss_keys"] == meta["loss_keys"]
     errs = {}
     grad_tol = tol if grad_tol is None else grad_tol
     for key, ref in fix.items():

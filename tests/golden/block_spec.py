@@ -138,3 +138,60 @@ def wire_heads(transformer, mlp_cls, contrastive_cls):
 def transformer_text_dict(inp, dtype=torch.float64, device="cpu"):
     return {"encoded_text": inp["text"].to(device, dtype), "text_token_mask": inp["token_mask"].to(device),
             "position_ids": inp["pos_ids"].to(device), "text_self_attention_masks": inp["text_sa"].to(device)}
+
+
+# ---------------------------------------------------------------- criterion
+# cfg_odvg.py:92-104 costs / coefficients; matcher call groundingdino.py:545
+MATCHER = dict(cost_class=1.0, cost_bbox=5.0, cost_giou=2.0, focal_alpha=0.25)
+FOCAL_ALPHA, FOCAL_GAMMA = 0.25, 2.0
+CRIT_QUERIES = 30
+
+
+def criterion_weight_dict(dec_layers=2):
+    """build_groundingdino's weight dict (groundingdino.py:764-795) for
+    cfg_odvg with dec_layers decoder layers and two-stage interm losses."""
+    base = {"loss_ce": 2.0, "loss_bbox": 5.0, "loss_giou": 2.0}
+    wd = dict(base)
+    for i in range(dec_layers - 1):
+        wd.update({f"{k}_{i}": v for k, v in base.items()})
+    wd.update({f"{k}_interm": v for k, v in base.items()})
+    return wd
+
+
+def criterion_inputs(tokenizer):
+    cat_list = [["cat", "traffic light", "dog"], ["person", "umbrella"]]
+    captions = [" . ".join(c) + " ." for c in cat_list]
+    token = tokenizer(captions, padding="longest", return_tensors="pt")
+    t = token["input_ids"].shape[1]
+    text_mask = torch.zeros(2, 256, dtype=torch.bool)
+    text_mask[:, :t] = token["attention_mask"].bool()
+    g = _gen("input:crit_boxes")
+    targets = []  # fp32, as the data pipeline produces them
+    for labels in ([0, 1, 2, 0], [0, 1, 1]):
+        k = len(labels)
+        c = 0.2 + 0.6 * torch.rand(k, 2, generator=g, dtype=torch.float64)
+        wh = 0.05 + 0.25 * torch.rand(k, 2, generator=g, dtype=torch.float64)
+        targets.append({"boxes": torch.cat([c, wh], 1).float(), "labels": torch.as_tensor(labels, dtype=torch.long)})
+    return dict(cat_list=cat_list, captions=captions, token=token, text_mask=text_mask, targets=targets)
+
+
+def criterion_outputs(inp, device="cpu", dtype=torch.float32):
+    """Model-shaped outputs (final layer, one aux layer, two-stage interm)
+    built from leaf tensors: logits are -inf on padded tokens as
+    ContrastiveEmbed produces them, boxes are sigmoid(cxcywh)."""
+    mask = inp["text_mask"].to(device)
+    leaves = {}
+
+    def head(tag):
+        lg = rand((2, CRIT_QUERIES, 256), f"crit_logits_{tag}", 2.0).to(device, dtype).requires_grad_(True)
+        bx = rand((2, CRIT_QUERIES, 4), f"crit_boxes_{tag}").to(device, dtype).requires_grad_(True)
+        leaves[f"{tag}_logits"] = lg
+        leaves[f"{tag}_boxes"] = bx
+        return {"pred_logits": lg.masked_fill(~mask[:, None, :], float("-inf")), "pred_boxes": bx.sigmoid()}
+
+    out = head("final")
+    out["aux_outputs"] = [head("aux0")]
+    out["interm_outputs"] = head("interm")
+    out["text_mask"] = mask
+    out["token"] = inp["token"]
+    return out, leaves

@@ -4,7 +4,7 @@ Run in the build container (where /root/reference exists):
     python tests/golden/make_block_golden.py
 
 The reference's model files are imported by path inside a synthetic package
-(``_refgd``, __path__ = /root/reference/models/GroundingDINO), bypassing its
+(``_refmodels.GroundingDINO``, __path__ = the reference model directory), bypassing its
 package __init__ files, which pull in torchvision / mmcv / timm.  None of those
 are installed, so this script registers minimal in-memory stand-ins before the
 import:
@@ -40,6 +40,10 @@ from torch import nn
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+# the product's offline tokenizer produces the token batches the criterion
+# reads (bert-base-uncased cannot be fetched here); nothing else of the
+# product is imported
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "open-groundingdino_amd"))
 import block_spec as spec  # noqa: E402
 
 REF = "/root/reference"
@@ -81,6 +85,16 @@ def _load_path(name, path):
     return mod
 
 
+def _box_area(boxes):
+    return (boxes[:, 2] - boxes[:, 0]) * (boxes[:, 3] - boxes[:, 1])
+
+
+def _unavailable(what):
+    def f(*a, **k):
+        raise RuntimeError(f"{what} is not available in the golden generator")
+    return f
+
+
 def install_shims():
     import transformers  # noqa: F401  (must precede the torchvision stand-in: it probes find_spec)
 
@@ -90,7 +104,7 @@ def install_shims():
             trunc_normal_=lambda t, mean=0.0, std=1.0, a=-2.0, b=2.0: nn.init.trunc_normal_(t, mean, std, a, b))
     tv = _module("torchvision", __version__="0.20.0")
     tv.ops = _module("torchvision.ops")
-    tv.ops.boxes = _module("torchvision.ops.boxes")
+    tv.ops.boxes = _module("torchvision.ops.boxes", box_area=_box_area, nms=_unavailable("torchvision nms"))
     tv.ops.misc = _module("torchvision.ops.misc")
 
     pkg = _module("groundingdino")
@@ -99,12 +113,26 @@ def install_shims():
     util.__path__ = []
     pkg.util = util
     util.misc = _load_path("groundingdino.util.misc", os.path.join(REF, "util", "misc.py"))
+    util.box_ops = _load_path("groundingdino.util.box_ops", os.path.join(REF, "util", "box_ops.py"))
+    util.get_tokenlizer = _load_path("groundingdino.util.get_tokenlizer", os.path.join(REF, "util", "get_tokenlizer.py"))
+    # imported by groundingdino.py for inference / visualisation only; their
+    # real modules need slconfig (addict, yapf), cv2, matplotlib, pycocotools
+    util.utils = _module("groundingdino.util.utils", get_phrases_from_posmap=_unavailable("get_phrases_from_posmap"))
+    util.visualizer = _module("groundingdino.util.visualizer", COCOVisualizer=_unavailable("COCOVisualizer"))
+    util.vl_utils = _module("groundingdino.util.vl_utils",
+                            create_positive_map_from_span=_unavailable("create_positive_map_from_span"))
+    top_util = _module("util")  # matcher.py imports util.box_ops
+    top_util.__path__ = []
+    top_util.box_ops = util.box_ops
+    sys.modules["util.box_ops"] = util.box_ops
 
-    refgd = _module("_refgd")
+    models = _module("_refmodels")
+    models.__path__ = [os.path.join(REF, "models")]
+    refgd = _module("_refmodels.GroundingDINO")
     refgd.__path__ = [REF_GD]
-    bb = _module("_refgd.backbone")
+    bb = _module("_refmodels.GroundingDINO.backbone", build_backbone=_unavailable("build_backbone"))
     bb.__path__ = [os.path.join(REF_GD, "backbone")]
-    local_msda = _load_path("_refgd.ms_deform_attn", os.path.join(REF_GD, "ms_deform_attn.py"))
+    local_msda = _load_path("_refmodels.GroundingDINO.ms_deform_attn", os.path.join(REF_GD, "ms_deform_attn.py"))
 
     class MMCVMultiScaleDeformableAttention(local_msda.MultiScaleDeformableAttention):
         def __init__(self, embed_dims=256, num_heads=8, num_levels=4, num_points=4, im2col_step=64,
@@ -130,12 +158,15 @@ def install_shims():
 def load_reference():
     install_shims()
     import importlib
+    p = "_refmodels.GroundingDINO."
     return types.SimpleNamespace(
-        fuse=importlib.import_module("_refgd.fuse_modules"),
-        utils=importlib.import_module("_refgd.utils"),
-        transformer=importlib.import_module("_refgd.transformer"),
-        swin=importlib.import_module("_refgd.backbone.swin_transformer"),
-        pos=importlib.import_module("_refgd.backbone.position_encoding"),
+        fuse=importlib.import_module(p + "fuse_modules"),
+        utils=importlib.import_module(p + "utils"),
+        transformer=importlib.import_module(p + "transformer"),
+        swin=importlib.import_module(p + "backbone.swin_transformer"),
+        pos=importlib.import_module(p + "backbone.position_encoding"),
+        matcher=importlib.import_module(p + "matcher"),
+        gd=importlib.import_module(p + "groundingdino"),
         misc=sys.modules["groundingdino.util.misc"],
     )
 
@@ -259,8 +290,25 @@ def case_transformer(ref):
                  "msda_semantics": "mmcv (dropout(output_proj(.)) + identity), dropout inactive (eval)"}
 
 
+def case_criterion(ref):
+    from gdino_amd.tokenizer import OfflineBertTokenizer
+    inp = spec.criterion_inputs(OfflineBertTokenizer())
+    matcher = ref.matcher.HungarianMatcher(**spec.MATCHER)
+    crit = ref.gd.SetCriterion(matcher, spec.criterion_weight_dict(), spec.FOCAL_ALPHA, spec.FOCAL_GAMMA,
+                               ["labels", "boxes"])
+    outputs, leaves = spec.criterion_outputs(inp, dtype=torch.float32)  # the label maps are fp32
+    losses = crit(outputs, inp["targets"], inp["cat_list"], inp["captions"])
+    wd = crit.weight_dict
+    total = sum(losses[k] * wd[k] for k in losses if k in wd)
+    total.backward()
+    res = {"loss." + k: np.array(float(v)) for k, v in losses.items()}
+    res["total"] = np.array(float(total))
+    res.update({"grad." + k: _np(v.grad) for k, v in leaves.items()})
+    return res, {"loss_keys": sorted(losses.keys())}
+
+
 CASES = {"biattn": case_biattn, "swin": case_swin, "pos": case_pos, "contrastive": case_contrastive,
-         "proposals": case_proposals, "transformer": case_transformer}
+         "proposals": case_proposals, "transformer": case_transformer, "criterion": case_criterion}
 
 
 def main(names=None):

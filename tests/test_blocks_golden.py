@@ -28,3 +28,11 @@ def test_block_matches_reference_fp64(name):
     with oracle_msda():
         errs = compare(name, "cpu", torch.float64, tol=1e-9)
     assert errs
+
+
+def test_criterion_matches_reference_fp32():
+    """SetCriterion + HungarianMatcher (groundingdino.py:405-639,
+    matcher.py:47-120): every loss term of the final, aux and interm heads
+    and the gradients w.r.t. logits and boxes, fp32 as in training."""
+    errs = compare("criterion", "cpu", torch.float32, tol=1e-5, grad_tol=1e-5)
+    assert errs["total"] < 1e-5

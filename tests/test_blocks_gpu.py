@@ -19,3 +19,8 @@ def test_block_matches_reference_fp32_on_gpu(name):
     _lib.lib()  # the HIP library must load (fails loudly otherwise)
     errs = compare(name, "cuda", torch.float32, tol=1e-3, grad_tol=1e-3)
     assert errs
+
+
+def test_criterion_matches_reference_on_gpu():
+    errs = compare("criterion", "cuda", torch.float32, tol=1e-4, grad_tol=1e-4)
+    assert errs["total"] < 1e-4
