@@ -24,18 +24,16 @@
  *   gd_runtime_info   <- get_cuda_version
  *                        models/GroundingDINO/csrc/vision.cpp:11-51,
  *                        models/GroundingDINO/csrc/cuda_version.cu
- *   gd_window_attn_*  <- WindowAttention.forward core (q*scale@k^T + rel-pos
- *                        bias + shift mask, softmax, @v)
- *                        models/GroundingDINO/backbone/swin_transformer.py:134-174
- *   gd_attn_*         <- scaled-dot-product attention with additive mask, used
- *                        by BERT self-attention (bertwarper.py:141-152 via HF
- *                        BertSelfAttention), the text enhancer
- *                        (transformer_vanilla.py:101-123) and the decoder
- *                        self / text cross attention (transformer.py:907-920)
- *   gd_biattn_*       <- BiMultiHeadAttention.forward core
- *                        models/GroundingDINO/fuse_modules.py:162-246
- *   gd_contrastive_*  <- ContrastiveEmbed.forward
- *                        models/GroundingDINO/utils.py:242-273
+ *   gd_biattn_softmax_fwd / _bwd / _workspace_bytes
+ *                     <- BiMultiHeadAttention.forward softmax chain (global
+ *                        max shift, +-5e4 clamps, column max, -inf masks, the
+ *                        two softmaxes) and its autograd backward
+ *                        models/GroundingDINO/fuse_modules.py:174-217
+ *
+ * Not (yet) in this ABI version — these run as hipBLASLt GEMMs / PyTorch
+ * SDPA compositions on the device: Swin window attention
+ * (swin_transformer.py:134-174), BERT / text-enhancer / decoder attention,
+ * ContrastiveEmbed (utils.py:242-273).
  */
 #ifndef GDINO_AMD_H
 #define GDINO_AMD_H

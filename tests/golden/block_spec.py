@@ -30,6 +30,16 @@ TRANSFORMER = dict(d_model=256, nhead=8, num_queries=30, num_encoder_layers=2, n
                    use_transformer_ckpt=False, use_text_cross_attention=True, text_dropout=0.0,
                    fusion_dropout=0.0, fusion_droppath=0.0)
 LEVELS = [(6, 8), (3, 4), (2, 2), (1, 1)]
+
+# real configurations for the state-dict compatibility fixture
+STATE_DICT_SWINS = {
+    "swin_T_224_1k": dict(pretrain_img_size=224, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
+                          window_size=7, out_indices=(1, 2, 3)),
+    "swin_B_384_22k": dict(pretrain_img_size=384, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+                           window_size=12, out_indices=(1, 2, 3)),
+}
+STATE_DICT_TRANSFORMER = dict(TRANSFORMER, num_encoder_layers=6, num_decoder_layers=6, dim_feedforward=2048,
+                              num_queries=900)
 TEXT_LEN = 13
 
 

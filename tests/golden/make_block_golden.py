@@ -307,8 +307,25 @@ def case_criterion(ref):
     return res, {"loss_keys": sorted(losses.keys())}
 
 
+def case_statedict(ref):
+    """State-dict keys and shapes (parameters and buffers) of the reference
+    modules at the real configurations: Swin-T / Swin-B-384 backbones and the
+    cfg_odvg Transformer (6+6 layers, 900 queries) with its heads wired."""
+    res = {}
+    meta = {}
+    for name, cfg in spec.STATE_DICT_SWINS.items():
+        sd = ref.swin.SwinTransformer(**cfg).state_dict()
+        meta[name] = {k: list(v.shape) for k, v in sd.items()}
+    t = ref.transformer.Transformer(**spec.STATE_DICT_TRANSFORMER)
+    spec.wire_heads(t, ref.utils.MLP, ref.utils.ContrastiveEmbed)
+    meta["transformer_cfg_odvg"] = {k: list(v.shape) for k, v in t.state_dict().items()}
+    res["n_keys"] = np.array([len(v) for v in meta.values()])
+    return res, {"state_dicts": meta}
+
+
 CASES = {"biattn": case_biattn, "swin": case_swin, "pos": case_pos, "contrastive": case_contrastive,
-         "proposals": case_proposals, "transformer": case_transformer, "criterion": case_criterion}
+         "proposals": case_proposals, "transformer": case_transformer, "criterion": case_criterion,
+         "statedict": case_statedict}
 
 
 def main(names=None):

@@ -36,3 +36,21 @@ def test_criterion_matches_reference_fp32():
     and the gradients w.r.t. logits and boxes, fp32 as in training."""
     errs = compare("criterion", "cpu", torch.float32, tol=1e-5, grad_tol=1e-5)
     assert errs["total"] < 1e-5
+
+
+def test_state_dicts_match_reference_at_real_configs():
+    """Every parameter AND buffer key, with its shape, of the reference's
+    Swin-T, Swin-B-384 and cfg_odvg Transformer (+ heads): checkpoints load
+    across with strict=True."""
+    from block_harness import fixture, spec
+    from models.GroundingDINO.backbone.swin_transformer import SwinTransformer
+    from models.GroundingDINO.transformer import Transformer
+    from models.GroundingDINO.utils import MLP, ContrastiveEmbed
+    _, meta = fixture("statedict")
+    ref = meta["state_dicts"]
+    for name, cfg in spec.STATE_DICT_SWINS.items():
+        mine = {k: list(v.shape) for k, v in SwinTransformer(**cfg).state_dict().items()}
+        assert mine == ref[name], name
+    t = Transformer(**spec.STATE_DICT_TRANSFORMER)
+    spec.wire_heads(t, MLP, ContrastiveEmbed)
+    assert {k: list(v.shape) for k, v in t.state_dict().items()} == ref["transformer_cfg_odvg"]
