@@ -51,3 +51,16 @@ def paired_generalized_box_iou(boxes1, boxes2):
     rb2 = torch.maximum(boxes1[:, 2:], boxes2[:, 2:])
     hull = (rb2 - lt2).clamp(min=0).prod(-1)
     return iou - (hull - union) / (hull + 1e-6)
+
+
+def generalized_box_iou_batched(boxes1, boxes2):
+    """GIoU of xyxy boxes with leading batch dims: boxes1 [..., N, 4],
+    boxes2 [..., M, 4] (broadcastable leading dims) -> [..., N, M]; same
+    formula and epsilons as generalized_box_iou."""
+    a1, a2 = box_area(boxes1), box_area(boxes2)
+    b1, b2 = boxes1[..., :, None, :], boxes2[..., None, :, :]
+    inter = (torch.minimum(b1[..., 2:], b2[..., 2:]) - torch.maximum(b1[..., :2], b2[..., :2])).clamp(min=0).prod(-1)
+    union = a1[..., :, None] + a2[..., None, :] - inter
+    iou = inter / (union + 1e-6)
+    hull = (torch.maximum(b1[..., 2:], b2[..., 2:]) - torch.minimum(b1[..., :2], b2[..., :2])).clamp(min=0).prod(-1)
+    return iou - (hull - union) / (hull + 1e-6)

@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
+from gdino_amd.conv import GemmConv2d
 from gdino_amd import kernels
 from gdino_amd.misc import DropPath, NestedTensor, to_2tuple, trunc_normal_
 
@@ -216,7 +217,7 @@ class PatchEmbed(nn.Module):
         self.patch_size = to_2tuple(patch_size)
         self.in_chans = in_chans
         self.embed_dim = embed_dim
-        self.proj = nn.Conv2d(in_chans, embed_dim, kernel_size=self.patch_size, stride=self.patch_size)
+        self.proj = GemmConv2d(in_chans, embed_dim, kernel_size=self.patch_size, stride=self.patch_size)
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
 
     def forward(self, x):

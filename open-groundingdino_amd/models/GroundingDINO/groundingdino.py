@@ -26,6 +26,8 @@ Host-path changes (same values, fewer syncs — SURVEY §7 hard part 5):
 from __future__ import annotations
 
 import copy
+
+import numpy as np
 from typing import List
 
 import torch
@@ -33,6 +35,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from gdino_amd import box_ops
+from gdino_amd.conv import GemmConv2d
 from gdino_amd.misc import (NestedTensor, get_world_size, inverse_sigmoid, is_dist_avail_and_initialized,
                             nested_tensor_from_tensor_list)
 from gdino_amd.tokenizer import get_pretrained_language_model, get_tokenlizer
@@ -81,17 +84,17 @@ class GroundingDINO(nn.Module):
             projs = []
             chans = list(backbone.num_channels)
             for c in chans:
-                projs.append(nn.Sequential(nn.Conv2d(c, hidden_dim, kernel_size=1), nn.GroupNorm(32, hidden_dim)))
+                projs.append(nn.Sequential(GemmConv2d(c, hidden_dim, kernel_size=1), nn.GroupNorm(32, hidden_dim)))
             in_c = chans[-1]
             for _ in range(num_feature_levels - len(chans)):
-                projs.append(nn.Sequential(nn.Conv2d(in_c, hidden_dim, kernel_size=3, stride=2, padding=1),
+                projs.append(nn.Sequential(GemmConv2d(in_c, hidden_dim, kernel_size=3, stride=2, padding=1),
                                            nn.GroupNorm(32, hidden_dim)))
                 in_c = hidden_dim
             self.input_proj = nn.ModuleList(projs)
         else:
             assert two_stage_type == "no", "two_stage_type should be no if num_feature_levels=1 !!!"
             self.input_proj = nn.ModuleList([nn.Sequential(
-                nn.Conv2d(backbone.num_channels[-1], hidden_dim, kernel_size=1), nn.GroupNorm(32, hidden_dim))])
+                GemmConv2d(backbone.num_channels[-1], hidden_dim, kernel_size=1), nn.GroupNorm(32, hidden_dim))])
 
         self.backbone = backbone
         self.aux_loss = aux_loss
@@ -322,24 +325,36 @@ class SetCriterion(nn.Module):
             labels = torch.arange(len(cat_list[j]))
             label_maps.append(create_positive_map(token[j], labels, cat_list[j], caption[j]).to(device))
 
-        # every (layer, image) matching problem of this step -> one D2H copy
         heads = [("", outputs)]
         for i, aux in enumerate(outputs.get("aux_outputs", [])):
             heads.append((f"_{i}", aux))
         if "interm_outputs" in outputs:
             heads.append(("_interm", outputs["interm_outputs"]))
-        problems = []
-        for _, o in heads:
-            for j in range(bs):
-                problems.append((o["pred_logits"][j], o["pred_boxes"][j], targets[j]["labels"],
-                                 targets[j]["boxes"].to(device), label_maps[j]))
-        all_indices = self.matcher.match_many(problems)
 
         num_boxes = torch.as_tensor([float(sum(len(t["labels"]) for t in targets))], device=device)
         if is_dist_avail_and_initialized():
             torch.distributed.all_reduce(num_boxes)
         num_boxes = torch.clamp(num_boxes / get_world_size(), min=1)[0]
 
+        if self._can_batch(heads, targets):
+            losses, indices_list = self._forward_batched(heads, outputs, targets, label_maps, num_boxes, device)
+        else:
+            losses, indices_list = self._forward_per_head(heads, outputs, targets, label_maps, num_boxes, device)
+        if return_indices:
+            return losses, indices_list[1:] + indices_list[:1]
+        return losses
+
+    def _forward_per_head(self, heads, outputs, targets, label_maps, num_boxes, device):
+        """The reference's loop (groundingdino.py:553-636): per head, match,
+        build the one-hot token targets, compute each loss.  All (head, image)
+        matching problems still share one device->host copy."""
+        bs = len(targets)
+        problems = []
+        for _, o in heads:
+            for j in range(bs):
+                problems.append((o["pred_logits"][j], o["pred_boxes"][j], targets[j]["labels"],
+                                 targets[j]["boxes"].to(device), label_maps[j]))
+        all_indices = self.matcher.match_many(problems)
         losses, indices_list = {}, []
         for h, (suffix, o) in enumerate(heads):
             indices = all_indices[h * bs:(h + 1) * bs]
@@ -350,9 +365,79 @@ class SetCriterion(nn.Module):
                 ld = self.get_loss(loss, o, targets, indices, num_boxes)
                 losses.update({k + suffix: v for k, v in ld.items()})
             indices_list.append(indices)
-        if return_indices:
-            return losses, indices_list[1:] + indices_list[:1]
-        return losses
+        return losses, indices_list
+
+    def _can_batch(self, heads, targets):
+        shp_l, shp_b = heads[0][1]["pred_logits"].shape, heads[0][1]["pred_boxes"].shape
+        return (set(self.losses) <= {"labels", "boxes"} and hasattr(self.matcher, "match_batched")
+                and all(o["pred_logits"].shape == shp_l and o["pred_boxes"].shape == shp_b for _, o in heads)
+                and max((len(t["labels"]) for t in targets), default=0) > 0)
+
+    def _forward_batched(self, heads, outputs, targets, label_maps, num_boxes, device):
+        """Every head at once (same losses as _forward_per_head, reference
+        :553-636): the H heads are stacked to [H, B, Q, .], the matcher builds
+        all H*B cost matrices in one pass (one device->host copy), and the
+        focal / L1 / GIoU losses are computed for all heads together and
+        reduced per head.  Replaces ~H x (matcher + 3 losses) small launches
+        with one set."""
+        H = len(heads)
+        logits = torch.stack([o["pred_logits"] for _, o in heads])          # [H, B, Q, 256]
+        boxes = torch.stack([o["pred_boxes"] for _, o in heads])            # [H, B, Q, 4]
+        sizes = [len(t["labels"]) for t in targets]
+        tgt_boxes = torch.nn.utils.rnn.pad_sequence([t["boxes"].to(device) for t in targets], batch_first=True)
+        maps = torch.nn.utils.rnn.pad_sequence(
+            [label_maps[b].index_select(0, t["labels"].to(device)) for b, t in enumerate(targets)], batch_first=True)
+        kmax = maps.shape[1]
+        valid = torch.as_tensor(np.arange(kmax)[None, :] < np.asarray(sizes)[:, None]).to(device, non_blocking=True)
+
+        indices = self.matcher.match_batched(logits, boxes, tgt_boxes, maps, valid, sizes)
+        flat = [(h, b, src, tgt) for h in range(H) for b, (src, tgt) in enumerate(indices[h])]
+        h_idx = np.concatenate([np.full(len(src), h) for h, _, src, _ in flat])
+        b_idx = np.concatenate([np.full(len(src), b) for _, b, src, _ in flat])
+        q_idx = np.concatenate([src.numpy() for _, _, src, _ in flat])
+        k_idx = np.concatenate([tgt.numpy() for _, _, _, tgt in flat])
+        n_pos = [max(sum(len(src) for src, _ in indices[h]), 1) for h in range(H)]
+        idx = torch.from_numpy(np.stack([h_idx, b_idx, q_idx, k_idx]).astype(np.int64)).to(device, non_blocking=True)
+        npos = torch.as_tensor(n_pos, dtype=torch.float32).to(device, non_blocking=True)
+        hi, bi, qi, ki = idx.unbind(0)
+
+        # token-level sigmoid focal loss (token_sigmoid_binary_focal_loss, :462-496)
+        t = torch.zeros(logits.shape, dtype=torch.float32, device=device)
+        t[hi, bi, qi] = maps[bi, ki].float()
+        keep = outputs["text_mask"][None, :, None, :]
+        x = torch.where(keep, logits.float(), torch.zeros((), device=device))
+        p = torch.sigmoid(x)
+        ce = F.binary_cross_entropy_with_logits(x, t, reduction="none")
+        p_t = p * t + (1 - p) * (1 - t)
+        fl = ce * ((1 - p_t) ** self.focal_gamma)
+        if self.focal_alpha >= 0:
+            fl = (self.focal_alpha * t + (1 - self.focal_alpha) * (1 - t)) * fl
+        loss_ce = torch.where(keep, fl, torch.zeros((), device=device)).sum((1, 2, 3)) / npos
+
+        # L1 + GIoU on the matched pairs (loss_boxes, :436-459)
+        src = boxes[hi, bi, qi].float()
+        tgt = tgt_boxes[bi, ki].float()
+        l1 = (src - tgt).abs()
+        giou = box_ops.paired_generalized_box_iou(box_ops.box_cxcywh_to_xyxy(src), box_ops.box_cxcywh_to_xyxy(tgt))
+        zeros = torch.zeros(H, dtype=torch.float32, device=device)
+        loss_bbox = zeros.index_add(0, hi, l1.sum(-1)) / num_boxes
+        loss_giou = zeros.index_add(0, hi, 1 - giou) / num_boxes
+        with torch.no_grad():
+            l1d = l1.detach()
+            loss_xy = zeros.index_add(0, hi, l1d[:, :2].sum(-1)) / num_boxes
+            loss_hw = zeros.index_add(0, hi, l1d[:, 2:].sum(-1)) / num_boxes
+
+        per = {"loss_ce": loss_ce.unbind(0), "loss_bbox": loss_bbox.unbind(0), "loss_giou": loss_giou.unbind(0),
+               "loss_xy": loss_xy.unbind(0), "loss_hw": loss_hw.unbind(0)}
+        order = (["loss_ce"] if "labels" in self.losses else []) + \
+                (["loss_bbox", "loss_giou", "loss_xy", "loss_hw"] if "boxes" in self.losses else [])
+        losses = {}
+        for h, (suffix, o) in enumerate(heads):
+            for k in order:
+                losses[k + suffix] = per[k][h]
+            if suffix:
+                o["text_mask"] = outputs["text_mask"]
+        return losses, indices
 
 
 def _nms(boxes, scores, iou_threshold):

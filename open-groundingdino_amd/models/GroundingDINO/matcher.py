@@ -19,6 +19,7 @@ import torch
 from scipy.optimize import linear_sum_assignment
 from torch import nn
 
+from gdino_amd import box_ops
 from gdino_amd.box_ops import box_cxcywh_to_xyxy, generalized_box_iou
 
 
@@ -73,6 +74,45 @@ class HungarianMatcher(nn.Module):
             except ValueError:  # reference falls back to min-sum (matcher.py:109-119)
                 i, j = mat.argmin(0), np.arange(n)
             out.append((torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)))
+        return out
+
+    @torch.no_grad()
+    def cost_batched(self, logits, boxes, tgt_boxes, maps, valid):
+        """All heads and images at once.
+
+        logits [H, B, Q, 256], boxes [H, B, Q, 4]; per image b the targets are
+        padded to K: tgt_boxes [B, K, 4], maps [B, K, 256] (raw positive-token
+        maps of each target's label), valid [B, K].  Returns C [H, B, Q, K];
+        entries of padded targets are garbage and must be ignored.  Same cost
+        as cost_matrix per (head, image)."""
+        p = logits.float().sigmoid()
+        a = self.focal_alpha
+        cls = a * ((1 - p) ** 2.0) * (-(p + 1e-8).log()) - (1 - a) * (p ** 2.0) * (-(1 - p + 1e-8).log())
+        m = maps.float()
+        m = m / m.sum(-1, keepdim=True)  # empty map -> NaN -> zeroed below, as the reference
+        m = torch.where(valid[..., None], m, torch.zeros((), device=m.device))
+        c_cls = torch.einsum("hbqt,bkt->hbqk", cls, m)
+        ob, tb = boxes.float(), tgt_boxes.float()
+        c_box = (ob[:, :, :, None, :] - tb[None, :, None, :, :]).abs().sum(-1)
+        c_giou = -box_ops.generalized_box_iou_batched(box_cxcywh_to_xyxy(ob), box_cxcywh_to_xyxy(tb)[None])
+        c = self.cost_bbox * c_box + self.cost_class * c_cls + self.cost_giou * c_giou
+        return torch.nan_to_num(c, nan=0.0, posinf=0.0, neginf=0.0)
+
+    @torch.no_grad()
+    def match_batched(self, logits, boxes, tgt_boxes, maps, valid, sizes):
+        """-> [[(src, tgt)] * B] * H, int64 CPU index tensors; one D2H copy."""
+        host = self.cost_batched(logits, boxes, tgt_boxes, maps, valid).cpu().numpy()
+        out = []
+        for h in range(host.shape[0]):
+            per = []
+            for b, n in enumerate(sizes):
+                mat = host[h, b, :, :n]
+                try:
+                    i, j = linear_sum_assignment(mat)
+                except ValueError:  # reference falls back to min-sum (matcher.py:109-119)
+                    i, j = mat.argmin(0), np.arange(n)
+                per.append((torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64)))
+            out.append(per)
         return out
 
     @torch.no_grad()

@@ -30,11 +30,19 @@ def test_block_matches_reference_fp64(name):
     assert errs
 
 
-def test_criterion_matches_reference_fp32():
+@pytest.mark.parametrize("batched", [True, False])
+def test_criterion_matches_reference_fp32(batched, monkeypatch):
     """SetCriterion + HungarianMatcher (groundingdino.py:405-639,
     matcher.py:47-120): every loss term of the final, aux and interm heads
-    and the gradients w.r.t. logits and boxes, fp32 as in training."""
+    and the gradients w.r.t. logits and boxes, fp32 as in training.  Both the
+    all-heads-batched path (default) and the reference-shaped per-head loop."""
+    from models.GroundingDINO.groundingdino import SetCriterion
+    taken = []
+    orig = SetCriterion._can_batch
+    monkeypatch.setattr(SetCriterion, "_can_batch",
+                        lambda self, h, t: taken.append(batched and orig(self, h, t)) or taken[-1])
     errs = compare("criterion", "cpu", torch.float32, tol=1e-5, grad_tol=1e-5)
+    assert taken == [batched]
     assert errs["total"] < 1e-5
 
 

@@ -1,0 +1,189 @@
+"""Count ATen dispatches (≈ device kernel launches) of one training step on
+CPU, by op, with the HIP-only ops routed to the oracle (their own internals are
+excluded from the count, each counts as one launch as on the GPU).
+
+The count does not depend on the image size, so a small image gives the same
+per-step launch profile as 800x1333.  CPU autocast (bf16) approximates CUDA
+autocast's cast insertion.  Usage:
+    python tools/count_ops.py [--top 40] [--no-autocast]
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd"), os.path.join(ROOT, "tests")]
+
+import torch  # noqa: E402
+from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
+
+# ops that launch no device kernel (metadata / views / host-side)
+_FREE = {"aten.view", "aten._unsafe_view", "aten.reshape", "aten.expand", "aten.permute", "aten.transpose",
+         "aten.t", "aten.squeeze", "aten.unsqueeze", "aten.select", "aten.slice", "aten.as_strided",
+         "aten.alias", "aten.detach", "aten.split", "aten.split_with_sizes", "aten.unbind", "aten.chunk",
+         "aten.narrow", "aten.flatten", "aten.unflatten", "aten.empty", "aten.empty_like", "aten.empty_strided",
+         "aten.lift_fresh", "aten._to_copy.no", "aten.size", "aten.stride", "aten.is_same_size",
+         "aten.sym_size", "aten.numel", "aten.dim", "aten._reshape_alias", "aten.new_empty",
+         "aten.new_empty_strided", "aten.view_as", "aten.movedim", "aten.diagonal", "aten.unfold",
+         "aten.set_", "aten.resize_", "aten.item", "aten._local_scalar_dense", "aten.is_nonzero",
+         "aten.equal", "aten.result_type"}
+
+
+class Counter(TorchDispatchMode):
+    def __init__(self):
+        super().__init__()
+        self.counts = collections.Counter()
+        self.paused = 0
+        self.phase = "fwd"
+        self.by_phase = collections.Counter()
+        self.phase_ops = collections.defaultdict(collections.Counter)
+        self.where = collections.Counter() if "--where" in sys.argv else None
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if not self.paused:
+            name = str(func.overloadpacket) if hasattr(func, "overloadpacket") else str(func)
+            name = name.replace("aten::", "aten.")
+            if name not in _FREE:
+                if name == "aten._to_copy":
+                    dt = kwargs.get("dtype")
+                    name = f"aten._to_copy[{args[0].dtype}->{dt}]"
+                self.counts[name] += 1
+                self.by_phase[self.phase] += 1
+                self.phase_ops[self.phase][name] += 1
+                if self.where is not None and self.phase in ("forward", "criterion"):
+                    import traceback
+                    for fr in reversed(traceback.extract_stack()[:-1]):
+                        if "open-groundingdino_amd" in fr.filename and "torch" not in fr.filename:
+                            rel = fr.filename.split("open-groundingdino_amd/")[-1]
+                            self.where[f"{rel}:{fr.lineno} {fr.line.strip()[:70]}"] += 1
+                            break
+        return func(*args, **(kwargs or {}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--no-autocast", action="store_true")
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=320)
+    ap.add_argument("--where", action="store_true", help="attribute fwd/criterion dispatches to source lines")
+    ap.add_argument("--phase", action="store_true", help="top ops per phase")
+    a = ap.parse_args()
+
+    import oracle_hooks
+    from gdino_amd import kernels, train
+    from gdino_amd.config import make_args
+
+    torch.manual_seed(0)
+    args = make_args(device="cpu", num_queries=900)
+    model, criterion, _, optimizer = train.build_training(args, "cpu")
+    model.train()
+    samples, targets, captions, cats = train.synthetic_batch(2, a.height, a.width, n_boxes=8, n_tokens=256,
+                                                             seed=0, device="cpu")
+    counter = Counter()
+
+    # HIP-only ops: one launch each for forward and one for backward, as on
+    # the GPU; the oracle restatements' own ops (forward and their autograd
+    # backward) are not counted
+    import models.GroundingDINO.ms_deform_attn as msda_mod
+    from oracle.blocks import bi_attention_ref
+
+    def counted(fn, tag):
+        class Op(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, *args):
+                ctx.args = args
+                counter.paused += 1
+                try:
+                    with torch.no_grad():
+                        out = fn(*args)
+                finally:
+                    counter.paused -= 1
+                counter.counts[tag + "_fwd"] += 1
+                ctx.tuple_out = isinstance(out, tuple)
+                return out
+
+            @staticmethod
+            def backward(ctx, *grads):
+                counter.paused += 1
+                try:
+                    with torch.enable_grad():
+                        args = [a.detach().requires_grad_(True) if torch.is_tensor(a) and a.is_floating_point()
+                                else a for a in ctx.args]
+                        out = fn(*args)
+                        outs = out if ctx.tuple_out else (out,)
+                        ins = [a for a in args if torch.is_tensor(a) and a.requires_grad]
+                        gs = iter(torch.autograd.grad(outs, ins, grads, allow_unused=True))
+                finally:
+                    counter.paused -= 1
+                counter.counts[tag + "_bwd"] += 1
+                return tuple(next(gs) if torch.is_tensor(a) and a.is_floating_point() else None
+                             for a in ctx.args)
+        return Op.apply
+
+    msda_op = counted(lambda *x: oracle_hooks._OracleMSDA.apply(*x), "gd.msda")
+
+    class CountedMSDA:
+        @staticmethod
+        def apply(*x):
+            return msda_op(*x)
+
+    bi_op = counted(lambda q, k, vv, vl, pv, pl: bi_attention_ref(q, k, vv, vl, pv, pl), "gd.biattn")
+
+    def counted_bi(q, k, vv, vl, pv=None, pl=None, p=0.0):
+        return bi_op(q, k, vv, vl, pv, pl)
+
+    prev = msda_mod.MSDeformAttnFunction
+    msda_mod.MSDeformAttnFunction = CountedMSDA
+    amp = None if a.no_autocast else torch.bfloat16
+
+    def step(c):
+        """train.train_step's phases, attributed separately (the optimizer is
+        excluded from the total: CPU AdamW is the per-parameter loop, the GPU
+        runs the fused multi-tensor kernel, ~25 launches)."""
+        c.phase = "forward"
+        with torch.autocast(device_type="cpu", dtype=amp or torch.bfloat16, enabled=amp is not None):
+            outputs = model(samples, captions=captions)
+            c.phase = "criterion"
+            loss_dict = criterion(outputs, targets, cats, captions)
+            wd = criterion.weight_dict
+            loss = sum(loss_dict[k] * wd[k] for k in loss_dict if k in wd)
+        optimizer.zero_grad(set_to_none=True)
+        c.phase = "backward"
+        loss.backward()
+        c.phase = "clip"
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1, foreach=True)
+        c.phase = "optimizer"
+        c.paused += 1
+        optimizer.step()
+        c.paused -= 1
+
+    try:
+        with kernels.override("bi_attention", counted_bi):
+            step(Counter())  # warm-up (caches)
+            with counter:
+                step(counter)
+    finally:
+        msda_mod.MSDeformAttnFunction = prev
+    total = sum(counter.counts.values())
+    casts = sum(v for k, v in counter.counts.items() if k.startswith("aten._to_copy"))
+    print(f"dispatches/step={total} (+~25 fused AdamW on GPU)  casts={casts}  by phase: {dict(counter.by_phase)}")
+    for k, v in counter.counts.most_common(a.top):
+        print(f"  {v:6d}  {k}")
+    if "--phase" in sys.argv:
+        for ph, c in counter.phase_ops.items():
+            print(f"--- {ph}")
+            for k, v in c.most_common(a.top):
+                print(f"  {v:6d}  {k}")
+    if counter.where is not None:
+        print("--- forward + criterion dispatches by source line")
+        for k, v in counter.where.most_common(a.top):
+            print(f"  {v:6d}  {k}")
+
+
+if __name__ == "__main__":
+    main()
