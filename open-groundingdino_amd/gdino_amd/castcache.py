@@ -1,0 +1,105 @@
+"""Per-parameter autocast weight cache.
+
+Under bf16 autocast every Linear casts its fp32 weight and bias to bf16 on
+each call. autocast's own cache lives only inside one autocast region, so the
+checkpoint recompute in the backward pass (Swin blocks and encoder layers,
+use_checkpoint / use_transformer_ckpt) casts them again. The frozen BERT's
+weights are also re-cast every step, and a slice of a parameter (the q/k/v
+rows of MultiheadAttention.in_proj_weight) is never cached at all. In total
+that is several hundred cast launches per step on a launch-bound step.
+
+``cached_cast(p, dtype)`` returns a bf16 copy of parameter ``p`` that stays
+valid while ``p._version`` is unchanged:
+
+* The optimizer's in-place update bumps the version, so the copy is
+  refreshed once per step.
+* Frozen weights are cast once.
+
+The copy is produced by the same ``p.to(dtype)`` autocast would run, so the
+numerics are bit-identical. When grad mode is on the copy is created with its
+cast node, so gradients reach the fp32 parameter through one ToCopyBackward
+per step.
+
+The cache is bypassed while a HIP graph is being captured: a graph must
+contain the cast, or its replays would read a stale copy after the optimizer
+step.
+"""
+from __future__ import annotations
+
+import os
+import weakref
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+ENABLED = os.environ.get("GDINO_CAST_CACHE", "1") != "0"
+_cache: dict = {}
+
+
+def autocast_dtype(x: torch.Tensor):
+    """The autocast lower-precision dtype active for x's device, or None
+    (also None when the cache is disabled: callers then fall back to
+    autocast's own casting)."""
+    if not ENABLED:
+        return None
+    dev = x.device.type
+    if dev not in ("cuda", "cpu") or not torch.is_autocast_enabled(dev):
+        return None
+    return torch.get_autocast_dtype(dev)
+
+
+def _capturing(p: torch.Tensor) -> bool:
+    return p.is_cuda and torch.cuda.is_current_stream_capturing()
+
+
+def cached_cast(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Callers only use this when ENABLED (otherwise they hand the fp32
+    parameter to autocast, whose own per-region cache then applies)."""
+    if p.dtype == dtype:
+        return p
+    grad = torch.is_grad_enabled() and p.requires_grad
+    if _capturing(p):
+        return p.to(dtype)
+    key = id(p)
+    ent = _cache.get(key)
+    if ent is not None and ent[0]() is p and ent[1] == p._version and ent[2] == dtype and ent[3] == grad:
+        return ent[4]
+    t = p.to(dtype)
+    _cache[key] = (weakref.ref(p), p._version, dtype, grad, t)
+    if len(_cache) > 8192:  # drop entries of freed parameters
+        for k in [k for k, v in _cache.items() if v[0]() is None]:
+            del _cache[k]
+    return t
+
+
+def clear() -> None:
+    _cache.clear()
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+    """F.linear with cached weight / bias casts under autocast."""
+    dt = autocast_dtype(x) if ENABLED else None
+    if dt is not None and weight.is_floating_point():
+        weight = cached_cast(weight, dt)
+        if bias is not None:
+            bias = cached_cast(bias, dt)
+    return F.linear(x, weight, bias)
+
+
+class CachedCastLinear(nn.Linear):
+    """nn.Linear using cached_cast under autocast (same parameters)."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)
+
+
+def install(model: nn.Module) -> int:
+    """Switch every plain nn.Linear of ``model`` to CachedCastLinear (class
+    swap: parameters, state dict and hooks are untouched).  Returns the count."""
+    n = 0
+    for m in model.modules():
+        if type(m) is nn.Linear:
+            m.__class__ = CachedCastLinear
+            n += 1
+    return n

@@ -28,6 +28,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from . import castcache
+
 
 def conv2d_gemm(x: torch.Tensor, weight: torch.Tensor, bias=None, stride=(1, 1), padding=(0, 0)):
     """F.conv2d(x, weight, bias, stride, padding) for dilation 1, groups 1,
@@ -48,6 +50,10 @@ def conv2d_gemm(x: torch.Tensor, weight: torch.Tensor, bias=None, stride=(1, 1),
         ho = (h + 2 * ph - kh) // sh + 1
         wo = (w + 2 * pw - kw) // sw + 1
         cols = F.unfold(x, (kh, kw), padding=(ph, pw), stride=(sh, sw))
+    dt = castcache.autocast_dtype(x)
+    if dt is not None:
+        weight = castcache.cached_cast(weight, dt)
+        bias = None if bias is None else castcache.cached_cast(bias, dt)
     out = torch.matmul(weight.reshape(o, c * kh * kw), cols)  # [B, O, Ho*Wo]
     if bias is not None:
         out = out + bias.to(out.dtype).view(1, o, 1)

@@ -16,6 +16,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from . import castcache
+
 
 def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor], b: int, h: int,
                 lq: int, lk: int, dtype) -> Optional[Tensor]:
@@ -72,18 +74,31 @@ class MultiheadAttention(nn.Module):
             nn.init.constant_(self.out_proj.bias, 0.0)
 
     def _project(self, query, key, value):
+        """q/k/v in-projections (nn.MultiheadAttention's in_proj layout).
+        Inputs that are the same tensor share one GEMM: q = k = x + pos in
+        the text enhancer and decoder self-attention, k = v = text in the
+        decoder's text cross-attention.  Under autocast the packed weight is
+        cast once per step (castcache) and sliced, instead of three casts of
+        its row blocks per call."""
         e = self.embed_dim
         w, bias = self.in_proj_weight, self.in_proj_bias
+        dt = castcache.autocast_dtype(query)
+        if dt is not None:
+            w = castcache.cached_cast(w, dt)
+            bias = None if bias is None else castcache.cached_cast(bias, dt)
+
+        def lin(x, r0, r1):
+            return F.linear(x, w[r0:r1], None if bias is None else bias[r0:r1])
+
         if query is key and key is value:
-            return F.linear(query, w, bias).chunk(3, dim=-1)
-        bq, bk, bv = (None, None, None) if bias is None else bias.split(e)
-        wq, wk, wv = w.split(e)
-        q = F.linear(query, wq, bq)
+            return lin(query, 0, 3 * e).chunk(3, dim=-1)
+        if query is key:
+            q, k = lin(query, 0, 2 * e).chunk(2, dim=-1)
+            return q, k, lin(value, 2 * e, 3 * e)
         if key is value:
-            k, v = F.linear(key, torch.cat([wk, wv]), None if bias is None else torch.cat([bk, bv])).chunk(2, -1)
-        else:
-            k, v = F.linear(key, wk, bk), F.linear(value, wv, bv)
-        return q, k, v
+            k, v = lin(key, e, 3 * e).chunk(2, dim=-1)
+            return lin(query, 0, e), k, v
+        return lin(query, 0, e), lin(key, e, 2 * e), lin(value, 2 * e, 3 * e)
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=False, attn_mask=None,
                 average_attn_weights=True, is_causal=False):

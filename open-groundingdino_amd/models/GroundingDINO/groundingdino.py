@@ -34,7 +34,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from gdino_amd import box_ops
+from gdino_amd import box_ops, castcache
 from gdino_amd.conv import GemmConv2d
 from gdino_amd.misc import (NestedTensor, get_world_size, inverse_sigmoid, is_dist_avail_and_initialized,
                             nested_tensor_from_tensor_list)
@@ -531,6 +531,7 @@ def build_groundingdino(args):
     criterion.to(torch.device(args.device))
     post = {"bbox": PostProcess(num_select=args.num_select, text_encoder_type=args.text_encoder_type,
                                 nms_iou_threshold=args.nms_iou_threshold, args=args)}
+    castcache.install(model)  # cached bf16 weight casts under autocast (bit-identical)
     return model, criterion, post
 
 

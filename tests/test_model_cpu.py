@@ -152,3 +152,40 @@ def test_mha_matches_torch_multihead_attention():
     m3 |= torch.eye(12, dtype=torch.bool)
     tiled = (~m3).repeat(4, 1, 1)
     torch.testing.assert_close(mine(q, q, q, attn_mask=tiled)[0], ref(q, q, q, attn_mask=tiled)[0])
+
+
+def test_cast_cache_is_bit_identical_under_autocast(built):
+    """gdino_amd.castcache (one bf16 cast per parameter per step, reused by the
+    checkpoint recompute and by the frozen BERT) must not change a single bit
+    of the loss or of any gradient relative to plain autocast casting."""
+    from gdino_amd import castcache
+    from gdino_amd.train import synthetic_batch
+    args, model, criterion, *_ = built
+    samples, targets, caps, cats = synthetic_batch(2, 128, 160, n_boxes=3, n_tokens=40, seed=1, device="cpu")
+    model.train()
+    assert any(isinstance(m, castcache.CachedCastLinear) for m in model.modules())
+
+    def run(enabled):
+        castcache.ENABLED = enabled
+        castcache.clear()
+        torch.manual_seed(7)
+        for p in model.parameters():
+            p.grad = None
+        with oracle_msda():  # the checkpoint recompute in backward runs MSDA again
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                out = model(samples, captions=caps)
+                ld = criterion(out, targets, cats, caps)
+                loss = sum(ld[k] * criterion.weight_dict[k] for k in ld if k in criterion.weight_dict)
+            loss.backward()
+        return loss.detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    try:
+        l0, g0 = run(False)
+        l1, g1 = run(True)
+    finally:
+        castcache.ENABLED = True
+        castcache.clear()
+    assert torch.equal(l0, l1)
+    assert g0.keys() == g1.keys() and len(g0) > 100
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
