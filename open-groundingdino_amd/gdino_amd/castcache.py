@@ -34,6 +34,11 @@ import torch.nn.functional as F
 from torch import nn
 
 ENABLED = os.environ.get("GDINO_CAST_CACHE", "1") != "0"
+# one GEMM for Linears that read the same input (linear_shared_input)
+FUSE_SHARED_INPUT = os.environ.get("GDINO_FUSE_PROJ", "1") != "0"
+# tests: fuse also without autocast (native dtype), to pin the fused path
+# against the fp64 reference goldens
+FUSE_WITHOUT_AUTOCAST = False
 _cache: dict = {}
 
 
@@ -103,3 +108,36 @@ def install(model: nn.Module) -> int:
             m.__class__ = CachedCastLinear
             n += 1
     return n
+
+
+def _cached_cat(params, dtype):
+    """bf16 concatenation (dim 0) of several parameters, cached like
+    cached_cast; gradients reach each parameter through the cat's split."""
+    ps = tuple(params)
+    if _capturing(ps[0]):
+        return torch.cat([p.to(dtype) for p in ps])
+    grad = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
+    key = ("cat",) + tuple(id(p) for p in ps)
+    vers = tuple(p._version for p in ps)
+    ent = _cache.get(key)
+    if ent is not None and all(r() is p for r, p in zip(ent[0], ps)) and ent[1] == vers and ent[2] == dtype \
+            and ent[3] == grad:
+        return ent[4]
+    t = torch.cat([p.to(dtype) for p in ps])
+    _cache[key] = (tuple(weakref.ref(p) for p in ps), vers, dtype, grad, t)
+    return t
+
+
+def linear_shared_input(x: torch.Tensor, layers):
+    """[layer(x) for layer in layers] for nn.Linear layers reading the same
+    input.  Under autocast with the cache on, one GEMM against the cached
+    concatenated bf16 weight (x is cast once); otherwise the plain per-layer
+    calls.  Parameters are untouched (state dict unchanged)."""
+    dt = autocast_dtype(x)
+    if dt is None and FUSE_WITHOUT_AUTOCAST:
+        dt = x.dtype
+    if dt is None or not FUSE_SHARED_INPUT or any(m.bias is None for m in layers):
+        return [m(x) for m in layers]
+    w = _cached_cat([m.weight for m in layers], dt)
+    b = _cached_cat([m.bias for m in layers], dt)
+    return list(F.linear(x, w, b).split([m.out_features for m in layers], dim=-1))

@@ -12,6 +12,7 @@ import torch
 import torch.nn as nn
 
 from gdino_amd import kernels
+from gdino_amd import castcache
 from gdino_amd.misc import DropPath
 
 
@@ -52,10 +53,11 @@ class BiMultiHeadAttention(nn.Module):
         """v [B, S, v_dim], l [B, T, l_dim]; masks True = padding."""
         b, s, _ = v.shape
         t = l.shape[1]
-        q = self._heads(self.v_proj(v) * self.scale)
-        k = self._heads(self.l_proj(l))
-        vv = self._heads(self.values_v_proj(v))
-        vl = self._heads(self.values_l_proj(l))
+        # projections sharing an input run as one GEMM on the training path
+        qv, vv = castcache.linear_shared_input(v, (self.v_proj, self.values_v_proj))
+        kl, vl = castcache.linear_shared_input(l, (self.l_proj, self.values_l_proj))
+        q = self._heads(qv * self.scale)
+        k, vv, vl = self._heads(kl), self._heads(vv), self._heads(vl)
         p = self.dropout if self.training else 0.0
         out_v, out_l = kernels.bi_attention(q, k, vv, vl, attention_mask_v, attention_mask_l, p)
         out_v = out_v.transpose(1, 2).reshape(b, s, self.embed_dim)

@@ -32,6 +32,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn.init import constant_, xavier_uniform_
 
+from gdino_amd import castcache
+
 from .ops.functions.ms_deform_attn_func import MSDeformAttnFunction
 
 
@@ -93,8 +95,9 @@ def msda_attend(mod, query, value, reference_points, spatial_shapes, level_start
     if key_padding_mask is not None:
         value = value.masked_fill(key_padding_mask[..., None], 0.0)
     value = value.view(bs, num_value, num_heads, -1)
-    offsets = mod.sampling_offsets(query).view(bs, num_query, num_heads, num_levels, num_points, 2)
-    attn = mod.attention_weights(query).view(bs, num_query, num_heads, num_levels * num_points)
+    offsets, attn = castcache.linear_shared_input(query, (mod.sampling_offsets, mod.attention_weights))
+    offsets = offsets.reshape(bs, num_query, num_heads, num_levels, num_points, 2)
+    attn = attn.reshape(bs, num_query, num_heads, num_levels * num_points)
     attn = attn.to(_loc_dtype(attn)).softmax(-1).view(bs, num_query, num_heads, num_levels, num_points)
     loc = sampling_locations_from(reference_points, offsets, spatial_shapes, num_points)
     if value.dtype == torch.float16:  # kernels run fp32 / bf16 / fp64 value

@@ -30,6 +30,18 @@ def test_block_matches_reference_fp64(name):
     assert errs
 
 
+@pytest.mark.parametrize("name", ["biattn", "transformer"])
+def test_fused_projections_match_reference_fp64(name, monkeypatch):
+    """The shared-input projection fusion (castcache.linear_shared_input:
+    MSDA offsets+weights, BiAttention v/values_v and l/values_l as one GEMM)
+    forced on in fp64: identical to the reference to 1e-9."""
+    from gdino_amd import castcache
+    monkeypatch.setattr(castcache, "FUSE_WITHOUT_AUTOCAST", True)
+    with oracle_msda():
+        errs = compare(name, "cpu", torch.float64, tol=1e-9)
+    assert errs
+
+
 @pytest.mark.parametrize("batched", [True, False])
 def test_criterion_matches_reference_fp32(batched, monkeypatch):
     """SetCriterion + HungarianMatcher (groundingdino.py:405-639,

@@ -165,14 +165,15 @@ def test_cast_cache_is_bit_identical_under_autocast(built):
     model.train()
     assert any(isinstance(m, castcache.CachedCastLinear) for m in model.modules())
 
-    def run(enabled):
+    def run(enabled, fuse=False, amp=True):
         castcache.ENABLED = enabled
+        castcache.FUSE_SHARED_INPUT = fuse
         castcache.clear()
         torch.manual_seed(7)
         for p in model.parameters():
             p.grad = None
         with oracle_msda():  # the checkpoint recompute in backward runs MSDA again
-            with torch.autocast("cpu", dtype=torch.bfloat16):
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=amp):
                 out = model(samples, captions=caps)
                 ld = criterion(out, targets, cats, caps)
                 loss = sum(ld[k] * criterion.weight_dict[k] for k in ld if k in criterion.weight_dict)
@@ -182,10 +183,22 @@ def test_cast_cache_is_bit_identical_under_autocast(built):
     try:
         l0, g0 = run(False)
         l1, g1 = run(True)
+        l2, g2 = run(True, fuse=True)
+        lf, gf = run(True, amp=False)
     finally:
         castcache.ENABLED = True
+        castcache.FUSE_SHARED_INPUT = True
         castcache.clear()
     assert torch.equal(l0, l1)
-    assert g0.keys() == g1.keys() and len(g0) > 100
+    assert g0.keys() == g1.keys() == g2.keys() and len(g0) > 100
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+    # shared-input projections as one GEMM: same math (pinned at 1e-9 in fp64
+    # by test_blocks_golden), GEMM blocking may round differently in bf16 ->
+    # must stay within the bf16-vs-fp32 noise of the unfused path
+    def rel(a, b):
+        return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+    assert abs(float(l2) - float(l0)) <= 1e-2 * abs(float(l0))
+    noise = max(rel(g0[n], gf[n]) for n in gf)
+    fused = max(rel(g2[n], gf[n]) for n in gf)
+    assert fused <= 1.25 * noise + 0.02, (fused, noise)

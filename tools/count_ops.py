@@ -32,6 +32,9 @@ _FREE = {"aten.view", "aten._unsafe_view", "aten.reshape", "aten.expand", "aten.
          "aten.equal", "aten.result_type"}
 
 
+_OP_FILTER = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--op=")]
+
+
 class Counter(TorchDispatchMode):
     def __init__(self):
         super().__init__()
@@ -54,7 +57,8 @@ class Counter(TorchDispatchMode):
                 self.counts[name] += 1
                 self.by_phase[self.phase] += 1
                 self.phase_ops[self.phase][name] += 1
-                if self.where is not None and self.phase in ("forward", "criterion"):
+                if self.where is not None and self.phase in ("forward", "criterion") and (
+                        not _OP_FILTER or any(f in name for f in _OP_FILTER)):
                     import traceback
                     for fr in reversed(traceback.extract_stack()[:-1]):
                         if "open-groundingdino_amd" in fr.filename and "torch" not in fr.filename:
@@ -72,6 +76,7 @@ def main():
     ap.add_argument("--width", type=int, default=320)
     ap.add_argument("--where", action="store_true", help="attribute fwd/criterion dispatches to source lines")
     ap.add_argument("--phase", action="store_true", help="top ops per phase")
+    ap.add_argument("--op", action="append", default=[], help="with --where: only these ops (substring)")
     a = ap.parse_args()
 
     import oracle_hooks
