@@ -53,6 +53,45 @@ def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor],
     return add
 
 
+PACKED_INPROJ = True
+
+
+class _PackedInProj(torch.autograd.Function):
+    """Two row blocks of a packed projection: ya = xa W[:split]^T + b[:split],
+    yb = xb W[split:]^T + b[split:].  Same GEMMs as two F.linear calls on
+    weight slices; the backward fills one packed dW / db with mm(out=) /
+    sum(out=) instead of autograd's zero-filled slice gradients + add."""
+
+    @staticmethod
+    def forward(ctx, w, b, xa, xb, split):
+        ctx.save_for_backward(w, xa, xb)
+        ctx.split = split
+        return F.linear(xa, w[:split], b[:split]), F.linear(xb, w[split:], b[split:])
+
+    @staticmethod
+    def backward(ctx, dya, dyb):
+        w, xa, xb = ctx.saved_tensors
+        sp = ctx.split
+        e = w.shape[1]
+        if dya is None:
+            dya = torch.zeros(*xa.shape[:-1], sp, dtype=w.dtype, device=w.device)
+        if dyb is None:
+            dyb = torch.zeros(*xb.shape[:-1], w.shape[0] - sp, dtype=w.dtype, device=w.device)
+        ga, gb = dya.reshape(-1, sp), dyb.reshape(-1, w.shape[0] - sp)
+        dxa = (ga @ w[:sp]).view(xa.shape) if ctx.needs_input_grad[2] else None
+        dxb = (gb @ w[sp:]).view(xb.shape) if ctx.needs_input_grad[3] else None
+        dw = db = None
+        if ctx.needs_input_grad[0]:
+            dw = torch.empty_like(w)
+            torch.mm(ga.t(), xa.reshape(-1, e), out=dw[:sp])
+            torch.mm(gb.t(), xb.reshape(-1, e), out=dw[sp:])
+        if ctx.needs_input_grad[1]:
+            db = torch.empty(w.shape[0], dtype=w.dtype, device=w.device)
+            torch.sum(ga, 0, out=db[:sp])
+            torch.sum(gb, 0, out=db[sp:])
+        return dw, db, dxa, dxb, None
+
+
 class MultiheadAttention(nn.Module):
     def __init__(self, embed_dim, num_heads, dropout=0.0, bias=True, batch_first=False):
         super().__init__()
@@ -78,20 +117,30 @@ class MultiheadAttention(nn.Module):
         Inputs that are the same tensor share one GEMM: q = k = x + pos in
         the text enhancer and decoder self-attention, k = v = text in the
         decoder's text cross-attention.  Under autocast the packed weight is
-        cast once per step (castcache) and sliced, instead of three casts of
-        its row blocks per call."""
+        cast once per step (castcache) and the two GEMMs run in
+        _PackedInProj, whose backward writes the packed [3E, E] gradient
+        directly (no zero-filled gradient per weight slice)."""
         e = self.embed_dim
         w, bias = self.in_proj_weight, self.in_proj_bias
+        if query is key and key is value:
+            return castcache.linear(query, w, bias).chunk(3, dim=-1)
         dt = castcache.autocast_dtype(query)
         if dt is not None:
             w = castcache.cached_cast(w, dt)
             bias = None if bias is None else castcache.cached_cast(bias, dt)
+            if bias is not None and PACKED_INPROJ and (query is key or key is value):
+                split = 2 * e if query is key else e
+                xa, xb = (query, value) if query is key else (query, key)
+                ya, yb = _PackedInProj.apply(w, bias, xa.to(dt), xb.to(dt), split)
+                if query is key:
+                    q, k = ya.chunk(2, dim=-1)
+                    return q, k, yb
+                k, v = yb.chunk(2, dim=-1)
+                return ya, k, v
 
         def lin(x, r0, r1):
             return F.linear(x, w[r0:r1], None if bias is None else bias[r0:r1])
 
-        if query is key and key is value:
-            return lin(query, 0, 3 * e).chunk(3, dim=-1)
         if query is key:
             q, k = lin(query, 0, 2 * e).chunk(2, dim=-1)
             return q, k, lin(value, 2 * e, 3 * e)
