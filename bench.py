@@ -49,7 +49,22 @@ def parse():
     ap.add_argument("--backbone", default="swin_T_224_1k")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--tunableop", default=None, metavar="CSV",
+                    help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
     return ap.parse_args()
+
+
+def use_tunableop(path):
+    """PyTorch TunableOp with a committed solution table (tools/tune_gemms.py
+    writes it): picks per-shape hipBLASLt solutions, e.g. split-K for the
+    long-K weight-gradient GEMMs, instead of the default heuristic's first
+    choice.  Must run before the first GEMM."""
+    t = torch.cuda.tunable
+    t.enable(True)
+    t.tuning_enable(False)
+    t.set_filename(path, False)
+    if not t.read_file(path):
+        raise RuntimeError(f"TunableOp could not read {path}")
 
 
 def setup_dist(n):
@@ -117,6 +132,8 @@ def main():
     rank, world, local = setup_dist(a.gpus)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    if a.tunableop:
+        use_tunableop(a.tunableop)
     torch.manual_seed(1234 + rank)
 
     from gdino_amd import msda
