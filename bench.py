@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--backbone", default="swin_T_224_1k")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--graphs", action="store_true",
+                    help="replay forward_core (fwd+bwd) as HIP graphs (experimental, 1 GPU; DESIGN.md §7)")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
     return ap.parse_args()
@@ -151,6 +153,14 @@ def main():
             model, device_ids=[local], bucket_cap_mb=a.bucket_mb, static_graph=True)
     samples, targets, captions, cats = synthetic_batch(a.bs, a.height, a.width, n_boxes=8, n_tokens=256,
                                                        seed=1000 + rank, device=device)
+    if a.graphs:
+        if world > 1:
+            raise SystemExit("--graphs is single-GPU for now")
+        from gdino_amd import graphs
+        text, _ = model.prepare_text(captions, device)
+        graphs.capture(model, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
+                               text["text_token_mask"], text["self_masks"], text["position_ids"]))
+        torch.cuda.synchronize()
 
     for _ in range(a.warmup):
         train_step(model, criterion, optimizer, samples, targets, captions, cats)
@@ -210,6 +220,7 @@ def main():
                          "frac": achieved / HBM_PEAK, "traffic": None,
                          "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"]},
             "kernels": kernels,
+            "options": {"hip_graphs": bool(a.graphs), "tunableop": a.tunableop},
             "loss": loss_v,
         }
         if not a.no_cpu_baseline and world == 1:
