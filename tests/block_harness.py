@@ -163,9 +163,50 @@ def run_criterion(device="cpu", dtype=torch.float32):
     return res, {"loss_keys": sorted(losses.keys())}
 
 
+def run_model(device="cpu", dtype=torch.float64, with_losses=True):
+    """Product build_groundingdino on the model case (block_spec.MODEL_*)."""
+    import models.GroundingDINO.groundingdino as gd
+    from gdino_amd.config import make_args
+    from gdino_amd.misc import NestedTensor
+    from gdino_amd.tokenizer import OfflineBertTokenizer
+
+    def tiny_lm(_name):
+        from transformers import BertConfig, BertModel
+        return BertModel(BertConfig(**spec.TINY_BERT))
+
+    prev = gd.get_pretrained_language_model
+    gd.get_pretrained_language_model = tiny_lm
+    try:
+        torch.manual_seed(0)
+        model, crit, _ = gd.build_groundingdino(make_args(device="cpu", **spec.MODEL_OVERRIDES))
+    finally:
+        gd.get_pretrained_language_model = prev
+    ck = spec.fill_params(model.to(dtype))
+    model = model.to(device).eval()
+    inp = spec.model_inputs(OfflineBertTokenizer())
+    out = model(NestedTensor(inp["images"].to(device, dtype), inp["mask"].to(device)), captions=inp["captions"])
+    res = {"pred_logits": out["pred_logits"], "pred_boxes": out["pred_boxes"],
+           "aux0_logits": out["aux_outputs"][0]["pred_logits"], "aux0_boxes": out["aux_outputs"][0]["pred_boxes"],
+           "interm_logits": out["interm_outputs"]["pred_logits"],
+           "interm_boxes": out["interm_outputs"]["pred_boxes"], "text_mask": out["text_mask"]}
+    spec.model_surrogate(out, device, torch.float64).backward()
+    named = dict(model.named_parameters())
+    for name in spec.MODEL_PGRADS:
+        _store_pgrad(res, name, named[name].grad)
+    meta = {"weights_checksum": ck, "param_names": sorted(named.keys())}
+    if with_losses:
+        with torch.no_grad():
+            targets = [{"boxes": t["boxes"].to(device, dtype), "labels": t["labels"].to(device)}
+                       for t in inp["targets"]]
+            losses = crit(out, targets, inp["cat_list"], inp["captions"])
+        res.update({"loss." + k: v for k, v in losses.items()})
+        meta["loss_keys"] = sorted(losses.keys())
+    return res, meta
+
+
 RUNNERS = {"biattn": run_biattn, "swin": run_swin, "pos": run_pos, "contrastive": run_contrastive,
            "proposals": run_proposals, "transformer": run_transformer,
-           "criterion": run_criterion}
+           "criterion": run_criterion, "model": run_model}
 
 
 def compare(name, device="cpu", dtype=torch.float64, tol=1e-9, grad_tol=None, skip=()):
@@ -174,28 +215,35 @@ def compare(name, device="cpu", dtype=torch.float64, tol=1e-9, grad_tol=None, sk
     fp32, so they are held to max(tol, 1e-6)."""
     fix, meta = fixture(name)
     runner = RUNNERS[name]
-    res, my_meta = runner(device, dtype, fix) if name == "proposals" else runner(device, dtype)
+    if name == "proposals":
+        res, my_meta = runner(device, dtype, fix)
+    elif name == "model":
+        res, my_meta = runner(device, dtype, with_losses=not any(k.startswith("loss.") for k in skip))
+    else:
+        res, my_meta = runner(device, dtype)
     if "weights_checksum" in meta:
         assert abs(my_meta["weights_checksum"] - meta["weights_checksum"]) <= 1e-9 * meta["weights_checksum"], \
             "parameter names/shapes differ from the reference"
     if "param_names" in meta:
         assert my_meta["param_names"] == meta["param_names"]
-    if "loss_keys" in meta:
+    if "loss_keys" in meta and "loss_keys" in my_meta:
         assert my_meta["loss_keys"] == meta["loss_keys"]
     errs = {}
     grad_tol = tol if grad_tol is None else grad_tol
     for key, ref in fix.items():
-        if key in ("memory", "mask") or key in skip:
+        if key in ("memory", "mask") or key in skip or any(key.startswith(p) for p in skip if p.endswith(".")):
             continue
         assert key in res, f"{name}: product produced no '{key}'"
         mine = res[key]
-        if key.startswith("mask"):
+        if key.startswith("mask") or key == "text_mask":
             assert np.array_equal(np.asarray(mine.cpu()), ref), key
             continue
         e = rel_err(mine, ref)
         errs[key] = e
         lim = grad_tol if ("grad" in key) else tol
-        if key.startswith("pgrad.") or ref.dtype == np.float32:
-            lim = max(lim, 1e-6)  # stored (or produced by the reference) in fp32
+        if key.startswith("pgrad.") or key.startswith("loss.") or ref.dtype == np.float32:
+            # stored in fp32, or computed in fp32 by the reference itself (the
+            # contrastive logits and the focal loss over them are fp32)
+            lim = max(lim, 1e-6)
         assert e <= lim, f"{name}.{key}: rel err {e:.3e} > {lim:.1e}"
     return errs

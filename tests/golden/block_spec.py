@@ -205,3 +205,45 @@ def criterion_outputs(inp, device="cpu", dtype=torch.float32):
     out["text_mask"] = mask
     out["token"] = inp["token"]
     return out, leaves
+
+
+# ---------------------------------------------------------------- full model
+# build_groundingdino(make_args(**MODEL_OVERRIDES)) on both sides, with a
+# small random BERT (TINY_BERT) instead of bert-base (same code path; keeps
+# the fixture generation fast) and the offline tokenizer.
+MODEL_OVERRIDES = dict(enc_layers=2, dec_layers=2, num_queries=30, dim_feedforward=256, use_checkpoint=False,
+                       use_transformer_ckpt=False, label_list=["cat", "traffic light", "dog", "person", "umbrella"])
+TINY_BERT = dict(hidden_size=96, num_hidden_layers=2, num_attention_heads=2, intermediate_size=192)
+MODEL_PGRADS = ("backbone.0.patch_embed.proj.weight", "backbone.0.layers.1.blocks.0.attn.qkv.weight",
+                "input_proj.0.0.weight", "input_proj.3.0.weight", "input_proj.3.1.weight", "feat_map.weight",
+                "bert.encoder.layer.1.attention.self.query.weight", "transformer.level_embed",
+                "transformer.encoder.layers.0.self_attn.value_proj.weight",
+                "transformer.encoder.fusion_layers.0.attn.out_v_proj.weight",
+                "transformer.decoder.layers.1.ca_text.in_proj_weight", "transformer.decoder.bbox_embed.0.layers.0.weight",
+                "transformer.enc_out_bbox_embed.layers.2.weight", "transformer.tgt_embed.weight")
+
+
+def model_inputs(tokenizer):
+    inp = criterion_inputs(tokenizer)
+    x = rand((2, 3, 64, 96), "model_img")
+    mask = torch.zeros(2, 64, 96, dtype=torch.bool)
+    mask[1, :, 80:] = True
+    mask[1, 56:, :] = True
+    inp["images"] = x.masked_fill(mask[:, None], 0.0)
+    inp["mask"] = mask
+    return inp
+
+
+def model_surrogate(out, device="cpu", dtype=torch.float64):
+    """Fixed random linear functional of every model output (gradient
+    source that does not depend on Hungarian matching)."""
+    terms = [("final", out["pred_logits"], out["pred_boxes"]),
+             ("aux0", out["aux_outputs"][0]["pred_logits"], out["aux_outputs"][0]["pred_boxes"]),
+             ("interm", out["interm_outputs"]["pred_logits"], out["interm_outputs"]["pred_boxes"])]
+    total = 0.0
+    for tag, lg, bx in terms:
+        finite = torch.isfinite(lg)
+        glg = rand(lg.shape, f"model_g_logits_{tag}").to(device, lg.dtype)
+        total = total + (torch.where(finite, lg, torch.zeros((), device=device, dtype=lg.dtype)) * glg).sum().to(dtype)
+        total = total + (bx * rand(bx.shape, f"model_g_boxes_{tag}").to(device, bx.dtype)).sum().to(dtype)
+    return total

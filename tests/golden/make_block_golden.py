@@ -106,6 +106,9 @@ def install_shims():
     tv.ops = _module("torchvision.ops")
     tv.ops.boxes = _module("torchvision.ops.boxes", box_area=_box_area, nms=_unavailable("torchvision nms"))
     tv.ops.misc = _module("torchvision.ops.misc")
+    tv.models = _module("torchvision.models")  # backbone.py: ResNet path only
+    tv.models._utils = _module("torchvision.models._utils", IntermediateLayerGetter=_unavailable("IntermediateLayerGetter"))
+    tv._is_tracing = lambda: False  # misc.nested_tensor_from_tensor_list
 
     pkg = _module("groundingdino")
     pkg.__path__ = []
@@ -155,9 +158,30 @@ def install_shims():
     _module("mmcv.ops.multi_scale_deform_attn", MultiScaleDeformableAttention=MMCVMultiScaleDeformableAttention)
 
 
+def _tiny_language_model(_name):
+    """get_pretrained_language_model stand-in: a random-init HF BertModel of
+    block_spec.TINY_BERT, given the two transformers-4.x methods the
+    reference's BertModelWarper binds (bertwarper.py:24-30) and that 5.x
+    removed / changed: get_head_mask (returns [None] * n_layers for
+    head_mask=None) and get_extended_attention_mask(mask, shape, device)
+    (3rd argument was the device; [B,T,T] -> additive [B,1,T,T])."""
+    from transformers import BertConfig, BertModel
+    m = BertModel(BertConfig(**spec.TINY_BERT, attn_implementation="eager"))
+    orig = m.get_extended_attention_mask
+    m.get_head_mask = lambda head_mask, n_layers, *a, **k: [None] * n_layers
+    m.get_extended_attention_mask = lambda mask, shape, device=None: orig(mask, shape)
+    return m
+
+
 def load_reference():
     install_shims()
     import importlib
+    from gdino_amd.tokenizer import OfflineBertTokenizer
+    gtk = sys.modules["groundingdino.util.get_tokenlizer"]
+    gtk.get_tokenlizer = lambda name: OfflineBertTokenizer()  # bert-base-uncased cannot be fetched here
+    gtk.get_pretrained_language_model = _tiny_language_model
+    bb = sys.modules["_refmodels.GroundingDINO.backbone"]
+    bb.build_backbone = importlib.import_module("_refmodels.GroundingDINO.backbone.backbone").build_backbone
     p = "_refmodels.GroundingDINO."
     return types.SimpleNamespace(
         fuse=importlib.import_module(p + "fuse_modules"),
@@ -323,9 +347,40 @@ def case_statedict(ref):
     return res, {"state_dicts": meta}
 
 
+def case_model(ref):
+    """build_groundingdino -> forward (final / aux / interm outputs) ->
+    reference criterion losses, and parameter gradients of a fixed surrogate
+    of all outputs; fp64, eval mode."""
+    from gdino_amd.config import make_args
+    from gdino_amd.tokenizer import OfflineBertTokenizer
+    torch.manual_seed(0)
+    args = make_args(device="cpu", **spec.MODEL_OVERRIDES)
+    model, crit, _ = ref.gd.build_groundingdino(args)
+    model = model.double()
+    model.eval()
+    ck = spec.fill_params(model)
+    inp = spec.model_inputs(OfflineBertTokenizer())
+    out = model(ref.misc.NestedTensor(inp["images"], inp["mask"]), captions=inp["captions"])
+    res = {"pred_logits": _np(out["pred_logits"]), "pred_boxes": _np(out["pred_boxes"]),
+           "aux0_logits": _np(out["aux_outputs"][0]["pred_logits"]),
+           "aux0_boxes": _np(out["aux_outputs"][0]["pred_boxes"]),
+           "interm_logits": _np(out["interm_outputs"]["pred_logits"]),
+           "interm_boxes": _np(out["interm_outputs"]["pred_boxes"]), "text_mask": _np(out["text_mask"])}
+    spec.model_surrogate(out).backward()
+    named = dict(model.named_parameters())
+    for name in spec.MODEL_PGRADS:
+        _pgrad(res, name, named[name].grad)
+    with torch.no_grad():
+        targets = [{"boxes": t["boxes"].double(), "labels": t["labels"]} for t in inp["targets"]]
+        losses = crit(out, targets, inp["cat_list"], inp["captions"])
+    res.update({"loss." + k: np.array(float(v)) for k, v in losses.items()})
+    return res, {"weights_checksum": ck, "param_names": sorted(named.keys()), "loss_keys": sorted(losses.keys()),
+                 "note": "BERT = random-init HF BertModel(TINY_BERT) behind the reference BertModelWarper"}
+
+
 CASES = {"biattn": case_biattn, "swin": case_swin, "pos": case_pos, "contrastive": case_contrastive,
          "proposals": case_proposals, "transformer": case_transformer, "criterion": case_criterion,
-         "statedict": case_statedict}
+         "statedict": case_statedict, "model": case_model}
 
 
 def main(names=None):

@@ -74,3 +74,15 @@ def test_state_dicts_match_reference_at_real_configs():
     t = Transformer(**spec.STATE_DICT_TRANSFORMER)
     spec.wire_heads(t, MLP, ContrastiveEmbed)
     assert {k: list(v.shape) for k, v in t.state_dict().items()} == ref["transformer_cfg_odvg"]
+
+
+def test_full_model_matches_reference_fp64():
+    """build_groundingdino end to end against the reference's own
+    build_groundingdino (groundingdino.py:216-392, 726-806): final / aux /
+    interm logits and boxes, text mask, 14 parameter gradients (Swin,
+    input_proj, feat_map, BERT, fusion, text cross-attention, heads) and every
+    loss term of the reference criterion on those outputs; fp64, eval mode,
+    small random BERT on both sides (block_spec.TINY_BERT)."""
+    with oracle_msda():
+        errs = compare("model", "cpu", torch.float64, tol=1e-9)
+    assert errs["pred_logits"] < 1e-9

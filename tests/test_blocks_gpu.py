@@ -24,3 +24,11 @@ def test_block_matches_reference_fp32_on_gpu(name):
 def test_criterion_matches_reference_on_gpu():
     errs = compare("criterion", "cuda", torch.float32, tol=1e-4, grad_tol=1e-4)
     assert errs["total"] < 1e-4
+
+
+def test_full_model_matches_reference_on_gpu():
+    """End-to-end model outputs and parameter gradients on the HIP path (fp32)
+    vs the reference (fp64 fixture).  Loss terms are pinned on CPU only:
+    Hungarian ties could legitimately differ between fp32 and fp64 costs."""
+    errs = compare("model", "cuda", torch.float32, tol=1e-3, grad_tol=1e-3, skip=("loss.",))
+    assert errs
