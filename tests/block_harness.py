@@ -60,20 +60,20 @@ def run_biattn(device="cpu", dtype=torch.float64):
     return res, {"weights_checksum": ck}
 
 
-def run_swin(device="cpu", dtype=torch.float64):
+def run_swin(device="cpu", dtype=torch.float64, cfg=None, inputs=None, tag=""):
     from gdino_amd.misc import NestedTensor
     from models.GroundingDINO.backbone.swin_transformer import SwinTransformer
-    m = SwinTransformer(**spec.SWIN)
+    m = SwinTransformer(**(cfg or spec.SWIN))
     ck = spec.fill_params(m.to(dtype))
     m = m.to(device).eval()
-    inp = spec.swin_inputs()
+    inp = (inputs or spec.swin_inputs)()
     x = inp["x"].to(device, dtype).requires_grad_(True)
     outs = m(NestedTensor(x, inp["mask"].to(device)))
     res, loss = {}, 0.0
     for k, nt in outs.items():
         res[f"feat{k}"] = nt.tensors
         res[f"mask{k}"] = nt.mask
-        g = spec.rand(nt.tensors.shape, f"swin_g{k}").to(device, dtype)
+        g = spec.rand(nt.tensors.shape, f"swin{tag}_g{k}").to(device, dtype)
         loss = loss + (nt.tensors * g).sum()
     loss.backward()
     res["grad_x"] = x.grad
@@ -204,9 +204,14 @@ def run_model(device="cpu", dtype=torch.float64, with_losses=True):
     return res, meta
 
 
+def run_swin_b(device="cpu", dtype=torch.float64):
+    return run_swin(device, dtype, spec.SWIN_B, spec.swin_b_inputs, "_b")
+
+
 RUNNERS = {"biattn": run_biattn, "swin": run_swin, "pos": run_pos, "contrastive": run_contrastive,
            "proposals": run_proposals, "transformer": run_transformer,
-           "criterion": run_criterion, "model": run_model}
+           "criterion": run_criterion, "model": run_model,
+           "swin_b": run_swin_b}
 
 
 def compare(name, device="cpu", dtype=torch.float64, tol=1e-9, grad_tol=None, skip=()):

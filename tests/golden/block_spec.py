@@ -29,6 +29,8 @@ TRANSFORMER = dict(d_model=256, nhead=8, num_queries=30, num_encoder_layers=2, n
                    embed_init_tgt=True, use_text_enhancer=True, use_fusion_layer=True, use_checkpoint=False,
                    use_transformer_ckpt=False, use_text_cross_attention=True, text_dropout=0.0,
                    fusion_dropout=0.0, fusion_droppath=0.0)
+SWIN_B = dict(pretrain_img_size=384, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+              window_size=12, out_indices=(1, 2, 3), drop_path_rate=0.0)  # BASELINE config 5 backbone
 LEVELS = [(6, 8), (3, 4), (2, 2), (1, 1)]
 
 # real configurations for the state-dict compatibility fixture
@@ -91,6 +93,15 @@ def swin_inputs():
     mask[1, 80:, :] = True
     x = x.masked_fill(mask[:, None], 0.0)
     return dict(x=x, mask=mask)
+
+
+def swin_b_inputs():
+    """1 image 96x160: stage-0 tokens 24x40 -> the 12-window padding and
+    shift-mask paths are exercised at every stage."""
+    x = rand((1, 3, 96, 160), "img_swin_b")
+    mask = torch.zeros(1, 96, 160, dtype=torch.bool)
+    mask[0, :, 150:] = True
+    return dict(x=x.masked_fill(mask[:, None], 0.0), mask=mask)
 
 
 def phrase_text(bs=2, t=TEXT_LEN):

@@ -225,19 +225,20 @@ def case_biattn(ref):
     return out, {"weights_checksum": ck}
 
 
-def case_swin(ref):
+def case_swin(ref, cfg=None, inputs=None, tag=""):
     torch.manual_seed(0)
-    m = ref.swin.SwinTransformer(**spec.SWIN).double()
+    m = ref.swin.SwinTransformer(**(cfg or spec.SWIN)).double()
     m.eval()  # SwinTransformer.train returns None in the reference: no chaining
     ck = spec.fill_params(m)
-    inp = spec.swin_inputs()
+    inp = (inputs or spec.swin_inputs)()
     x = inp["x"].clone().requires_grad_(True)
     outs = m(ref.misc.NestedTensor(x, inp["mask"]))
     res, loss = {}, 0.0
     for k, nt in outs.items():
-        res[f"feat{k}"] = _np(nt.tensors)
+        # Swin-B feature maps are stored in fp32 (fixture size); held to 1e-6
+        res[f"feat{k}"] = nt.tensors.detach().float().numpy() if tag else _np(nt.tensors)
         res[f"mask{k}"] = _np(nt.mask)
-        g = spec.rand(nt.tensors.shape, f"swin_g{k}")
+        g = spec.rand(nt.tensors.shape, f"swin{tag}_g{k}")
         loss = loss + (nt.tensors * g).sum()
     loss.backward()
     res["grad_x"] = x.grad.float().numpy()
@@ -378,9 +379,14 @@ def case_model(ref):
                  "note": "BERT = random-init HF BertModel(TINY_BERT) behind the reference BertModelWarper"}
 
 
+def case_swin_b(ref):
+    return case_swin(ref, spec.SWIN_B, spec.swin_b_inputs, "_b")
+
+
 CASES = {"biattn": case_biattn, "swin": case_swin, "pos": case_pos, "contrastive": case_contrastive,
          "proposals": case_proposals, "transformer": case_transformer, "criterion": case_criterion,
-         "statedict": case_statedict, "model": case_model}
+         "statedict": case_statedict, "model": case_model,
+         "swin_b": case_swin_b}
 
 
 def main(names=None):

@@ -23,7 +23,7 @@ from block_harness import compare
 from oracle_hooks import oracle_msda
 
 
-@pytest.mark.parametrize("name", ["biattn", "swin", "pos", "contrastive", "proposals", "transformer"])
+@pytest.mark.parametrize("name", ["biattn", "swin", "swin_b", "pos", "contrastive", "proposals", "transformer"])
 def test_block_matches_reference_fp64(name):
     with oracle_msda():
         errs = compare(name, "cpu", torch.float64, tol=1e-9)

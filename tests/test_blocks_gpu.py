@@ -13,7 +13,7 @@ from block_harness import compare
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["biattn", "swin", "pos", "contrastive", "proposals", "transformer"])
+@pytest.mark.parametrize("name", ["biattn", "swin", "swin_b", "pos", "contrastive", "proposals", "transformer"])
 def test_block_matches_reference_fp32_on_gpu(name):
     from gdino_amd import _lib
     _lib.lib()  # the HIP library must load (fails loudly otherwise)

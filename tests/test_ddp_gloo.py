@@ -1,6 +1,6 @@
 """Data-parallel path on CPU: world_size-2 gloo, the full model wrapped in
 DDP exactly as bench.py / the reference main.py do (main.py:258-261), each
-rank a different synthetic batch.  Checks that the gradient all-reduce makes
+rank a different synthetic batch, three bf16-autocast train steps.  Checks that the gradient all-reduce makes
 every rank's gradients and post-step parameters identical, and that the
 criterion's num_boxes all-reduce (groundingdino.py:574-576) runs."""
 import os
@@ -39,7 +39,12 @@ def _worker(rank, world, port, q):
         samples, targets, caps, cats = synthetic_batch(1, 96, 128, n_boxes=2, n_tokens=20, seed=100 + rank,
                                                        device="cpu")
         with oracle_msda():
-            loss = train_step(ddp, criterion, opt, samples, targets, caps, cats, amp_dtype=None)
+            # bf16 autocast as in bench.py: exercises the cast cache, the fused
+            # projections and the packed in-projection under DDP; three steps
+            # so static_graph's recorded plan and the per-step cache refresh
+            # (optimizer updates bump parameter versions) are both used
+            for _ in range(3):
+                loss = train_step(ddp, criterion, opt, samples, targets, caps, cats, amp_dtype=torch.bfloat16)
         grads = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None])
         params = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
         ref_g, ref_p = grads.clone(), params.clone()
