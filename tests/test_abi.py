@@ -61,3 +61,18 @@ def test_product_refuses_cpu_tensors():
     attn = torch.ones(1, 1, 1, 1, 1)
     with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
         msda.ms_deform_attn_forward(v, shapes, lsi, loc, attn, 64)
+
+
+def test_msda_module_is_a_drop_in_for_the_reference_extension():
+    """replacing `import MultiScaleDeformableAttention as
+    MSDA` (ops/functions/ms_deform_attn_func.py:18) with `from gdino_amd
+    import msda as MSDA` works because the call shapes of :25-26 and :35-36
+    are accepted positionally."""
+    import inspect
+    from gdino_amd import msda
+    fwd = list(inspect.signature(msda.ms_deform_attn_forward).parameters.values())
+    bwd = list(inspect.signature(msda.ms_deform_attn_backward).parameters.values())
+    # reference passes 6 (fwd) / 7 (bwd) positional arguments, nothing else
+    assert len([p for p in fwd if p.default is inspect.Parameter.empty]) <= 6 <= len(fwd)
+    assert len([p for p in bwd if p.default is inspect.Parameter.empty]) <= 7 <= len(bwd)
+    assert [p.name for p in bwd[5:7]] == ["grad_output", "im2col_step"]
