@@ -1,0 +1,48 @@
+#!/usr/bin/env bash
+# One GPU session on a fresh MI355X box (run through gpurun from the repo root):
+#   gpurun --timeout 1200 -- bash tools/gpu_session.sh [core|tune|graphs]
+# Every GPU step has its own time limit and the steps are chained with &&:
+# the first failure ends the session (no retries, no further GPU work).
+# Logs and profiler output go to gpurun_out/ (copy the summaries that are to
+# be judged into profiles/ afterwards).
+set -euo pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+MODE="${1:-core}"
+T() { timeout -k 10 "$@"; }
+
+case "$MODE" in
+core)
+  # 1) parity on the HIP path, 2) the default bench line, 3) A/B of the
+  # host-overhead switches, 4) kernel trace of the default bench, 5/6) HBM
+  # traffic counters in their own passes (FETCH_SIZE and WRITE_SIZE do not
+  # fit one TCC pass; MI355X_MICROARCH.md "rocprofv3 PMC slots")
+  T 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/s_gpu_tests.log 2>&1 &&
+  T 600 python3 bench.py > gpurun_out/s_bench.log 2>&1 &&
+  GDINO_CAST_CACHE=0 GDINO_FUSE_PROJ=0 T 600 python3 bench.py --no-cpu-baseline \
+      > gpurun_out/s_bench_nocache.log 2>&1 &&
+  T 600 rocprofv3 --kernel-trace --stats -d gpurun_out/s_prof -o run -- \
+      python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > gpurun_out/s_prof.log 2>&1 &&
+  T 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/s_pmc_fetch -o run -- \
+      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_fetch.log 2>&1 &&
+  T 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/s_pmc_write -o run -- \
+      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_write.log 2>&1
+  ;;
+tune)
+  # TunableOp: tune the step's GEMM shapes, then bench with the table
+  T 900 python3 tools/tune_gemms.py --out tunableop/gdino_train_gfx950.csv > gpurun_out/s_tune.log 2>&1 &&
+  T 600 python3 bench.py --no-cpu-baseline --tunableop tunableop/gdino_train_gfx950.csv \
+      > gpurun_out/s_bench_tunable.log 2>&1
+  ;;
+graphs)
+  # HIP-graph replay (experimental; faulted in round 1 before MIOpen was
+  # removed from the captured region): run alone, in its own gpurun call
+  GDINO_GRAPH_DEBUG=1 T 600 python3 bench.py --no-cpu-baseline --graphs --steps 5 --warmup 2 \
+      > gpurun_out/s_bench_graphs.log 2>&1
+  ;;
+*)
+  echo "usage: $0 [core|tune|graphs]" >&2
+  exit 2
+  ;;
+esac
