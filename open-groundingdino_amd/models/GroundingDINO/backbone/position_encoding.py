@@ -5,13 +5,25 @@ import math
 import torch
 from torch import nn
 
+from gdino_amd.misc import device_const
 
-def _sine_channels(embed: torch.Tensor, num_feats: int, temperature: float) -> torch.Tensor:
-    """embed [B, H, W] -> [B, H, W, num_feats] interleaved sin/cos."""
-    idx = torch.arange(num_feats, dtype=torch.float32, device=embed.device)
-    dim_t = temperature ** (2 * torch.div(idx, 2, rounding_mode="floor") / num_feats)
-    pos = embed[..., None] / dim_t
-    return torch.stack((pos[..., 0::2].sin(), pos[..., 1::2].cos()), dim=4).flatten(3)
+
+def _dim_t(num_feats: int, temperature: float, device) -> torch.Tensor:
+    """temperature ** (2 * (i // 2) / num_feats), built once per device with
+    the device's arithmetic (the reference rebuilds it on every call)."""
+    def make():
+        idx = torch.arange(num_feats, dtype=torch.float32, device=device)
+        return temperature ** (2 * torch.div(idx, 2, rounding_mode="floor") / num_feats)
+    return device_const(("pos_dim_t", num_feats, float(temperature)), make, device)
+
+
+def _sine_yx(y: torch.Tensor, x: torch.Tensor, num_feats: int, temp_h: float, temp_w: float) -> torch.Tensor:
+    """y, x [B, H, W] -> [B, H, W, 2*num_feats]: (pos_y, pos_x) interleaved
+    sin/cos channels, both coordinates in one pass (same per-element math as
+    one embedding per coordinate + cat)."""
+    dims = torch.stack((_dim_t(num_feats, temp_h, y.device), _dim_t(num_feats, temp_w, y.device)))
+    pos = torch.stack((y, x), dim=-1)[..., None] / dims          # [B, H, W, 2, F]
+    return torch.stack((pos[..., 0::2].sin(), pos[..., 1::2].cos()), dim=-1).flatten(3)
 
 
 class PositionEmbeddingSineHW(nn.Module):
@@ -37,9 +49,7 @@ class PositionEmbeddingSineHW(nn.Module):
             eps = 1e-6
             y = y / (y[:, -1:, :] + eps) * self.scale
             x = x / (x[:, :, -1:] + eps) * self.scale
-        pos_x = _sine_channels(x, self.num_pos_feats, self.temperatureW)
-        pos_y = _sine_channels(y, self.num_pos_feats, self.temperatureH)
-        return torch.cat((pos_y, pos_x), dim=3).permute(0, 3, 1, 2)
+        return _sine_yx(y, x, self.num_pos_feats, self.temperatureH, self.temperatureW).permute(0, 3, 1, 2)
 
 
 class PositionEmbeddingSine(PositionEmbeddingSineHW):

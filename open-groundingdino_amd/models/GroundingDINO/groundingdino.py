@@ -322,8 +322,8 @@ class SetCriterion(nn.Module):
         bs = len(cat_list)
         label_maps = []
         for j in range(bs):
-            labels = torch.arange(len(cat_list[j]))
-            label_maps.append(create_positive_map(token[j], labels, cat_list[j], caption[j]).to(device))
+            label_maps.append(create_positive_map(token[j], range(len(cat_list[j])), cat_list[j], caption[j])
+                              .to(device))
 
         heads = [("", outputs)]
         for i, aux in enumerate(outputs.get("aux_outputs", [])):
@@ -539,8 +539,8 @@ def create_positive_map(tokenized, tokens_positive, cat_list, caption):
     """positive_map[i, j] = 1 iff label i's phrase covers token j
     (reference :808-855: first/last character of the phrase's first
     occurrence in the caption, end falling back 1-2 characters)."""
-    pm = torch.zeros((len(tokens_positive), 256), dtype=torch.float)
-    for j, label in enumerate(tokens_positive):
+    pm = np.zeros((len(tokens_positive), 256), dtype=np.float32)  # host array, one tensor at the end
+    for j, label in enumerate(tokens_positive.tolist() if torch.is_tensor(tokens_positive) else tokens_positive):
         name = cat_list[int(label)]
         start = caption.find(name)
         end = start + len(name) - 1
@@ -555,5 +555,5 @@ def create_positive_map(tokenized, tokens_positive, cat_list, caption):
                 break
         if beg_pos is None or end_pos is None or beg_pos < 0 or end_pos < 0 or beg_pos > end_pos:
             continue
-        pm[j, beg_pos:end_pos + 1].fill_(1)
-    return pm
+        pm[j, beg_pos:end_pos + 1] = 1.0
+    return torch.from_numpy(pm)

@@ -9,6 +9,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from gdino_amd.misc import device_const
+
 from gdino_amd import kernels
 from gdino_amd.misc import sigmoid_focal_loss  # noqa: F401  (re-export, reference utils.py:152)
 
@@ -20,8 +22,12 @@ def _get_clones(module, N, layer_share=False):
 
 
 def _dim_t(num_feats: int, temperature: float, device) -> Tensor:
-    idx = torch.arange(num_feats, dtype=torch.float32, device=device)
-    return temperature ** (2 * torch.div(idx, 2, rounding_mode="floor") / num_feats)
+    """temperature ** (2 * (i // 2) / num_feats), computed once per device
+    with the device's own arithmetic (as the reference computes it per call)."""
+    def make():
+        idx = torch.arange(num_feats, dtype=torch.float32, device=device)
+        return temperature ** (2 * torch.div(idx, 2, rounding_mode="floor") / num_feats)
+    return device_const(("dim_t", num_feats, float(temperature)), make, device)
 
 
 def _sin_cos(x: Tensor, dim_t: Tensor) -> Tensor:
@@ -44,14 +50,17 @@ def get_sine_pos_embed(pos_tensor: Tensor, num_pos_feats: int = 128, temperature
 def gen_sineembed_for_position(pos_tensor: Tensor) -> Tensor:
     """[nq, bs, 2|4] -> [nq, bs, 256|512]: (y, x[, w, h]) 128 feats each, T=1e4
     (reference utils.py:204-230)."""
-    dim_t = _dim_t(128, 10000, pos_tensor.device)
-    coords = pos_tensor * (2 * math.pi)
-    emb = [_sin_cos(coords[..., i], dim_t) for i in range(pos_tensor.size(-1))]
-    if pos_tensor.size(-1) == 2:
-        return torch.cat((emb[1], emb[0]), dim=-1)
-    if pos_tensor.size(-1) == 4:
-        return torch.cat((emb[1], emb[0], emb[2], emb[3]), dim=-1)
-    raise ValueError("Unknown pos_tensor shape(-1):{}".format(pos_tensor.size(-1)))
+    n = pos_tensor.size(-1)
+    if n not in (2, 4):
+        raise ValueError("Unknown pos_tensor shape(-1):{}".format(n))
+    dev = pos_tensor.device
+    dim_t = _dim_t(128, 10000, dev)
+    # all coordinates at once, in output order (y, x[, w, h]): same per-element
+    # arithmetic as one embedding per coordinate + cat
+    order = device_const(("sine_order", n), lambda: torch.tensor([1, 0, 2, 3][:n], device=dev), dev)
+    coords = (pos_tensor * (2 * math.pi)).index_select(-1, order)
+    v = coords[..., None] / dim_t
+    return torch.stack((v[..., 0::2].sin(), v[..., 1::2].cos()), dim=-1).flatten(-3)
 
 
 def gen_encoder_output_proposals(memory: Tensor, memory_padding_mask: Tensor, spatial_shapes: Tensor,
