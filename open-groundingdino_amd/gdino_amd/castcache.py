@@ -115,7 +115,7 @@ def _cached_cat(params, dtype):
     cached_cast; gradients reach each parameter through the cat's split."""
     ps = tuple(params)
     if _capturing(ps[0]):
-        return torch.cat([p.to(dtype) for p in ps])
+        return torch.cat(ps).to(dtype)
     grad = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
     key = ("cat",) + tuple(id(p) for p in ps)
     vers = tuple(p._version for p in ps)
@@ -123,7 +123,7 @@ def _cached_cat(params, dtype):
     if ent is not None and all(r() is p for r, p in zip(ent[0], ps)) and ent[1] == vers and ent[2] == dtype \
             and ent[3] == grad:
         return ent[4]
-    t = torch.cat([p.to(dtype) for p in ps])
+    t = torch.cat(ps).to(dtype)  # = cat of the casts, one cast kernel (and one in backward)
     _cache[key] = (tuple(weakref.ref(p) for p in ps), vers, dtype, grad, t)
     return t
 
