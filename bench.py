@@ -38,7 +38,7 @@ HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
 LEVELS_800 = [(100, 167), (50, 84), (25, 42), (13, 21)]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -53,7 +53,7 @@ def parse():
                     help="replay forward_core (fwd+bwd) as HIP graphs (experimental, 1 GPU; DESIGN.md §7)")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def use_tunableop(path):
@@ -129,11 +129,17 @@ def cpu_baseline(bs):
     }
 
 
-def main():
-    a = parse()
+def main(argv=None, device_type="cuda"):
+    """device_type="cpu" exists for tests/test_bench_contract.py only (the
+    HIP ops are then routed to the oracle by the test); the bench itself
+    always runs on cuda."""
+    a = parse(argv)
     rank, world, local = setup_dist(a.gpus)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+    on_gpu = device_type == "cuda"
+    device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    if on_gpu:
+        torch.cuda.set_device(device)
     if a.tunableop:
         use_tunableop(a.tunableop)
     torch.manual_seed(1234 + rank)
@@ -160,22 +166,22 @@ def main():
         text, _ = model.prepare_text(captions, device)
         graphs.capture(model, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
                                text["text_token_mask"], text["self_masks"], text["position_ids"]))
-        torch.cuda.synchronize()
+        sync()
 
     for _ in range(a.warmup):
         train_step(model, criterion, optimizer, samples, targets, captions, cats)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
 
     msda.timer = msda.LaunchTimer()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = train_step(model, criterion, optimizer, samples, targets, captions, cats)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

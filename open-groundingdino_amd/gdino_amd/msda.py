@@ -38,7 +38,8 @@ class LaunchTimer:
         self.records.append((kind, lq, nbytes, start, ev))
 
     def summary(self):
-        torch.cuda.synchronize()
+        if self.records:
+            torch.cuda.synchronize()
         out = {}
         for kind, lq, nbytes, s, e in self.records:
             d = out.setdefault((kind, lq), {"n": 0, "ms": 0.0, "bytes": nbytes})
