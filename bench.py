@@ -69,12 +69,13 @@ def use_tunableop(path):
         raise RuntimeError(f"TunableOp could not read {path}")
 
 
-def setup_dist(n):
+def setup_dist(n, on_gpu=True):
     if n <= 1 and "RANK" not in os.environ:
         return 0, 1, 0
     local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
-    torch.cuda.set_device(local)  # bind the device before RCCL creates its communicator
-    dist.init_process_group("nccl")
+    if on_gpu:
+        torch.cuda.set_device(local)  # bind the device before RCCL creates its communicator
+    dist.init_process_group("nccl" if on_gpu else "gloo")  # gloo: CPU contract test only
     return dist.get_rank(), dist.get_world_size(), local
 
 
@@ -134,8 +135,8 @@ def main(argv=None, device_type="cuda"):
     HIP ops are then routed to the oracle by the test); the bench itself
     always runs on cuda."""
     a = parse(argv)
-    rank, world, local = setup_dist(a.gpus)
     on_gpu = device_type == "cuda"
+    rank, world, local = setup_dist(a.gpus, on_gpu)
     device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     if on_gpu:
@@ -156,7 +157,7 @@ def main(argv=None, device_type="cuda"):
         # xGMI rings (fewer, larger all-reduces), launched as backward
         # produces them so RCCL overlaps the rest of the backward pass
         model = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local], bucket_cap_mb=a.bucket_mb, static_graph=True)
+            model, device_ids=[local] if on_gpu else None, bucket_cap_mb=a.bucket_mb, static_graph=True)
     samples, targets, captions, cats = synthetic_batch(a.bs, a.height, a.width, n_boxes=8, n_tokens=256,
                                                        seed=1000 + rank, device=device)
     if a.graphs:

@@ -37,3 +37,54 @@ def test_bench_prints_the_contract_json_line(capsys):
     cb = res["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
     assert cb["unit"].startswith("images/s")
+
+
+def _rank_worker(rank, world, port, q):
+    import contextlib
+    import io
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "open-groundingdino_amd")]
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(3)
+    import bench
+    from oracle_hooks import oracle_msda
+    buf = io.StringIO()
+    try:
+        with oracle_msda(), contextlib.redirect_stdout(buf):
+            bench.main(["--gpus", str(world), "--steps", "1", "--warmup", "1", "--height", "256", "--width", "320"],
+                       device_type="cpu")
+        q.put((rank, "ok", buf.getvalue()))
+    except Exception as e:  # noqa: BLE001 (reported to the parent)
+        q.put((rank, repr(e), buf.getvalue()))
+
+
+def test_bench_two_ranks_contract():
+    """The torchrun path the driver's scaling runs take (--gpus N, one rank per
+    device, DDP, barrier + max-over-ranks timing): two gloo ranks on CPU.
+    Rank 0 alone prints the line; value counts the images of all ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=900)
+    res = dict((r, (st, out)) for r, st, out in (q.get(timeout=5) for _ in range(2)))
+    assert all(p.exitcode == 0 for p in procs)
+    assert res[0][0] == "ok" and res[1][0] == "ok", res
+    assert not [ln for ln in res[1][1].splitlines() if ln.startswith("{")], "only rank 0 prints"
+    lines = [ln for ln in res[0][1].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    r0 = json.loads(lines[0])
+    assert r0["n_gpus"] == 2 and r0["config"]["parallelism"] == "dp2" and r0["config"]["global_batch"] == 4
+    assert abs(r0["value"] - 4 / (r0["ms_per_step"] / 1e3)) < 1e-6 * r0["value"]  # 2 images x 2 ranks per step
+    assert "cpu_baseline" not in r0  # rank 0 at N=1 only
