@@ -22,7 +22,7 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
 from gdino_amd.conv import GemmConv2d
-from gdino_amd import kernels
+from gdino_amd import castcache, kernels
 from gdino_amd.misc import DropPath, NestedTensor, to_2tuple, trunc_normal_
 
 
@@ -119,7 +119,14 @@ class SwinTransformerBlock(nn.Module):
         assert length == h * w, "input feature has wrong size"
         ws, sh = self.window_size, self.shift_size
         shortcut = x
-        x = self.norm1(x).view(b, h, w, c)
+        x = self.norm1(x)
+        dt = castcache.autocast_dtype(x)
+        if dt is not None:
+            # the qkv GEMM casts its input anyway: cast before the pad / roll /
+            # window-partition copies (exact in either dtype) so they move half
+            # the bytes; bit-identical to casting inside the Linear
+            x = x.to(dt)
+        x = x.view(b, h, w, c)
         pad_r, pad_b = (ws - w % ws) % ws, (ws - h % ws) % ws
         if pad_r or pad_b:
             x = F.pad(x, (0, 0, 0, pad_r, 0, pad_b))
