@@ -48,6 +48,26 @@ from .transformer import build_transformer
 from .utils import MLP, ContrastiveEmbed
 
 
+def prepare_text_host(tokenizer, special_tokens, max_text_len, captions):
+    """Tokenize the captions and build the sub-sentence masks on the host
+    (reference groundingdino.py:235-262: padding="longest", phrase-block
+    self-attention masks and position ids, truncation to max_text_len).
+    -> (dict of CPU tensors, tokenizer output)."""
+    tokenized = tokenizer(captions, padding="longest", return_tensors="pt")
+    self_masks, position_ids, _ = generate_masks_with_special_tokens_and_transfer_map(
+        tokenized, special_tokens, tokenizer)
+    tok = {k: v for k, v in tokenized.items()}
+    if self_masks.shape[1] > max_text_len:
+        self_masks = self_masks[:, :max_text_len, :max_text_len]
+        position_ids = position_ids[:, :max_text_len]
+        for k in ("input_ids", "attention_mask", "token_type_ids"):
+            tok[k] = tok[k][:, :max_text_len]
+    text = {"input_ids": tok["input_ids"], "token_type_ids": tok["token_type_ids"],
+            "text_token_mask": tok["attention_mask"].bool(), "self_masks": self_masks,
+            "position_ids": position_ids}
+    return text, tokenized
+
+
 class GroundingDINO(nn.Module):
     def __init__(self, backbone, transformer, num_queries, aux_loss=False, iter_update=False, query_dim=2,
                  num_feature_levels=1, nheads=8, two_stage_type="no", dec_pred_bbox_embed_share=True,
@@ -140,24 +160,16 @@ class GroundingDINO(nn.Module):
         self.refpoint_embed = nn.Embedding(use_num_queries, self.query_dim)
 
     # ------------------------------------------------------------------ text
-    def prepare_text(self, captions, device):
-        """Host side of the text path: tokenize, phrase masks / position ids
-        (numpy, no device syncs), truncate to max_text_len, move once.
+    def prepare_text(self, captions, device, prepared=None):
+        """Host side of the text path (tokenize, phrase masks / position ids,
+        truncate to max_text_len: prepare_text_host) and one move to the
+        device.  ``prepared`` = prepare_text_host's result computed elsewhere
+        (e.g. in DataLoader workers by gdino_amd.data.TextPreprocessor);
+        pinned tensors are copied asynchronously.
         -> (dict of device tensors, tokenizer output for the loss)."""
-        tokenized = self.tokenizer(captions, padding="longest", return_tensors="pt")
-        self_masks, position_ids, _ = generate_masks_with_special_tokens_and_transfer_map(
-            tokenized, self.specical_tokens, self.tokenizer)
-        n = self.max_text_len
-        tok = {k: v for k, v in tokenized.items()}
-        if self_masks.shape[1] > n:
-            self_masks = self_masks[:, :n, :n]
-            position_ids = position_ids[:, :n]
-            for k in ("input_ids", "attention_mask", "token_type_ids"):
-                tok[k] = tok[k][:, :n]
-        text = {"input_ids": tok["input_ids"], "token_type_ids": tok["token_type_ids"],
-                "text_token_mask": tok["attention_mask"].bool(), "self_masks": self_masks,
-                "position_ids": position_ids}
-        return {k: v.to(device) for k, v in text.items()}, tokenized
+        text, tokenized = prepared if prepared is not None else prepare_text_host(
+            self.tokenizer, self.specical_tokens, self.max_text_len, captions)
+        return {k: v.to(device, non_blocking=v.is_pinned()) for k, v in text.items()}, tokenized
 
     def encode_text(self, input_ids, token_type_ids, text_token_mask, self_masks, position_ids):
         """BERT + feat_map -> text_dict (groundingdino.py:259-287)."""
@@ -220,7 +232,7 @@ class GroundingDINO(nn.Module):
         if isinstance(samples, (list, torch.Tensor)):
             samples = nested_tensor_from_tensor_list(samples)
         device = samples.tensors.device
-        text, one_hot_token = self.prepare_text(captions, device)
+        text, one_hot_token = self.prepare_text(captions, device, kw.get("prepared_text"))
         core = self._graphed_core if getattr(self, "_graphed_core", None) is not None else self.forward_core
         (outputs_class, outputs_coord, text_mask, interm_class, interm_coord,
          init_box_proposal) = core(samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],

@@ -1,0 +1,159 @@
+"""ODVG data path (gdino_amd.data): dataset semantics of the reference's
+datasets/odvg.py:135-272, DETR-style transforms (datasets/transforms.py),
+collate, DataLoader-worker text preparation, and one model step fed from the
+loader.  Synthetic images and annotations (no dataset is on disk)."""
+import json
+import types
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from oracle_hooks import oracle_msda
+
+LABEL_MAP = {"0": "cat", "1": "dog", "2": "person", "3": "umbrella", "4": "traffic light", "5": "car"}
+
+
+@pytest.fixture(scope="module")
+def odvg_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("odvg")
+    rng = np.random.default_rng(0)
+    sizes = [(96, 64), (60, 80), (70, 50)]  # (w, h)
+    od, vg = [], []
+    for i, (w, h) in enumerate(sizes):
+        Image.fromarray(rng.integers(0, 255, (h, w, 3), dtype=np.uint8)).save(d / f"img{i}.png")
+        od.append({"filename": f"img{i}.png", "height": h, "width": w, "detection": {"instances": [
+            {"bbox": [2.0, 3.0, 20.0, 30.0], "label": 1, "category": "dog"},
+            {"bbox": [10.0, 5.0, w - 1.0, h - 2.0], "label": 4, "category": "traffic light"},
+            {"bbox": [0.0, 0.0, 8.0, 9.0], "label": 1, "category": "dog"}]}})
+        vg.append({"filename": f"img{i}.png", "height": h, "width": w, "grounding": {
+            "caption": "a man with an umbrella", "regions": [
+                {"bbox": [1.0, 1.0, 15.0, 25.0], "phrase": "a man"},
+                {"bbox": [5.0, 2.0, 30.0, 20.0], "phrase": "an umbrella"},
+                {"bbox": [3.0, 4.0, 9.0, 12.0], "phrase": "a man"}]}})
+    (d / "od.jsonl").write_text("\n".join(json.dumps(r) for r in od))
+    (d / "vg.jsonl").write_text("\n".join(json.dumps(r) for r in vg))
+    (d / "label_map.json").write_text(json.dumps(LABEL_MAP))
+    return d
+
+
+def test_od_caption_labels_and_negatives(odvg_dir):
+    from gdino_amd.data import ODVGDataset
+    ds = ODVGDataset(str(odvg_dir), str(odvg_dir / "od.jsonl"), str(odvg_dir / "label_map.json"), max_labels=4,
+                     seed=0)
+    assert ds.mode == "OD" and len(ds) == 3
+    img, t = ds[0]
+    assert img.size == (96, 64)
+    cap = t["cap_list"]
+    assert len(cap) == 4 and len(set(cap)) == 4 and {"dog", "traffic light"} <= set(cap)
+    assert t["caption"] == " . ".join(cap) + " ."
+    assert [cap[i] for i in t["labels"].tolist()] == ["dog", "traffic light", "dog"]
+    assert torch.equal(t["boxes"][0], torch.tensor([2.0, 3.0, 20.0, 30.0]))
+    assert t["size"].tolist() == [64, 96]
+    ds2 = ODVGDataset(str(odvg_dir), str(odvg_dir / "od.jsonl"), str(odvg_dir / "label_map.json"), max_labels=4,
+                      seed=0)
+    assert ds2[0][1]["caption"] == t["caption"]  # seeded -> reproducible
+
+
+def test_vg_unique_phrases(odvg_dir):
+    from gdino_amd.data import ODVGDataset
+    ds = ODVGDataset(str(odvg_dir), str(odvg_dir / "vg.jsonl"), seed=1)
+    assert ds.mode == "VG"
+    _, t = ds[1]
+    assert sorted(t["cap_list"]) == ["a man", "an umbrella"]
+    phrases = [t["cap_list"][i] for i in t["labels"].tolist()]
+    assert sorted(phrases) == ["a man", "a man", "an umbrella"]
+    assert t["boxes"].shape == (3, 4)
+
+
+@pytest.mark.parametrize("wh,size,max_size,expect", [
+    ((640, 480), 800, 1333, (800, 1066)),
+    ((2000, 500), 800, 1333, (333, 1332)),
+    ((800, 800), 800, 1333, (800, 800)),
+    ((480, 640), 512, None, (682, 512)),
+    ((100, 50), (30, 40), None, (40, 30)),
+])
+def test_resize_rule(wh, size, max_size, expect):
+    from gdino_amd.data.transforms import resize_size
+    assert resize_size(wh, size, max_size) == expect
+
+
+def test_box_transforms():
+    from gdino_amd.data import transforms as T
+    img = Image.fromarray(np.arange(40 * 60 * 3, dtype=np.uint8).reshape(40, 60, 3))
+    tgt = {"boxes": torch.tensor([[10.0, 5.0, 30.0, 25.0], [55.0, 30.0, 60.0, 40.0]]),
+           "labels": torch.tensor([0, 1]), "size": torch.tensor([40, 60])}
+    f, tf = T.hflip(img, tgt)
+    assert torch.equal(tf["boxes"][0], torch.tensor([30.0, 5.0, 50.0, 25.0]))
+    assert np.array_equal(np.asarray(f), np.asarray(img)[:, ::-1])
+    r, tr = T.resize(img, tgt, 20)  # shorter side 40 -> 20
+    assert r.size == (30, 20) and tr["size"].tolist() == [20, 30]
+    assert torch.allclose(tr["boxes"][0], torch.tensor([5.0, 2.5, 15.0, 12.5]))
+    c, tc = T.crop(img, tgt, (0, 0, 28, 40))  # second box falls outside -> dropped with its label
+    assert c.size == (40, 28) and tc["labels"].tolist() == [0]
+    assert torch.equal(tc["boxes"], torch.tensor([[10.0, 5.0, 30.0, 25.0]]))
+    x, tn = T.Compose([T.ToTensor(), T.Normalize()])(img, tgt)
+    assert x.shape == (3, 40, 60)
+    assert torch.allclose(tn["boxes"][0], torch.tensor([20 / 60, 15 / 40, 20 / 60, 20 / 40]))
+    mean = torch.tensor(T.IMAGENET_MEAN).view(3, 1, 1)
+    std = torch.tensor(T.IMAGENET_STD).view(3, 1, 1)
+    raw = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255).permute(2, 0, 1)
+    assert torch.allclose(x, (raw - mean) / std)
+
+
+def _small_args():
+    return types.SimpleNamespace(data_aug_scales=[96, 128], data_aug_max_size=192, data_aug_scales2_resize=[96],
+                                 data_aug_scales2_crop=[64, 96], max_labels=4)
+
+
+def test_loader_with_worker_text_preparation(odvg_dir):
+    from gdino_amd.data import ODVGCollator, TextPreprocessor, build_odvg
+    from gdino_amd.tokenizer import get_tokenlizer
+    from models.GroundingDINO.groundingdino import prepare_text_host
+    ds = build_odvg("train", _small_args(), {"root": str(odvg_dir), "anno": str(odvg_dir / "od.jsonl"),
+                                             "label_map": str(odvg_dir / "label_map.json")}, seed=3)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, num_workers=2, collate_fn=ODVGCollator(TextPreprocessor()),
+                                         persistent_workers=False)
+    samples, targets, prepared = next(iter(loader))
+    b, _, h, w = samples.tensors.shape
+    assert b == 2 and samples.mask.shape == (2, h, w)
+    for i, t in enumerate(targets):
+        hh, ww = t["size"].tolist()
+        assert not samples.mask[i, :hh, :ww].any() and samples.mask[i, hh:, :].all() and samples.mask[i, :, ww:].all()
+        assert ((t["boxes"] >= 0) & (t["boxes"] <= 1)).all()
+    tok = get_tokenlizer("bert-base-uncased")
+    ref_text, _ = prepare_text_host(tok, tok.convert_tokens_to_ids(["[CLS]", "[SEP]", ".", "?"]), 256,
+                                    [t["caption"] for t in targets])
+    text, tokenized = prepared
+    assert text.keys() == ref_text.keys()
+    for k in text:
+        assert torch.equal(text[k], ref_text[k]), k
+
+
+def test_model_step_from_loader(odvg_dir):
+    from gdino_amd.config import make_args
+    from gdino_amd.data import ODVGCollator, TextPreprocessor, build_odvg
+    from gdino_amd.train import build_training
+    ds = build_odvg("train", _small_args(), {"root": str(odvg_dir), "anno": str(odvg_dir / "od.jsonl"),
+                                             "label_map": str(odvg_dir / "label_map.json")}, seed=4)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, num_workers=0, collate_fn=ODVGCollator(TextPreprocessor()))
+    samples, targets, prepared = next(iter(loader))
+    torch.manual_seed(0)
+    model, criterion, _, opt = build_training(make_args(device="cpu", num_queries=50, enc_layers=1, dec_layers=2),
+                                              "cpu")
+    caps = [t["caption"] for t in targets]
+    cats = [t["cap_list"] for t in targets]
+    with oracle_msda():
+        model.eval()
+        with torch.no_grad():
+            a = model(samples, captions=caps, prepared_text=prepared)
+            b = model(samples, captions=caps)
+        assert torch.equal(a["pred_logits"], b["pred_logits"]) and torch.equal(a["pred_boxes"], b["pred_boxes"])
+        model.train()
+        out = model(samples, captions=caps, prepared_text=prepared)
+        ld = criterion(out, targets, cats, caps)
+        loss = sum(ld[k] * criterion.weight_dict[k] for k in ld if k in criterion.weight_dict)
+        loss.backward()
+    assert torch.isfinite(loss)
+    assert model.transformer.level_embed.grad is not None
