@@ -41,6 +41,11 @@ class NestedTensor:
     def decompose(self):
         return self.tensors, self.mask
 
+    def pin_memory(self):
+        """DataLoader(pin_memory=True) hook: page-locked host tensors, so the
+        host->device copy of the batch is asynchronous."""
+        return NestedTensor(self.tensors.pin_memory(), None if self.mask is None else self.mask.pin_memory())
+
     @property
     def device(self):
         return self.tensors.device

@@ -67,6 +67,9 @@ class TokenBatch(dict):
     def to(self, device):
         return TokenBatch({k: v.to(device) for k, v in self.items()}, self._items)
 
+    def pin_memory(self):
+        return TokenBatch({k: v.pin_memory() for k, v in self.items()}, self._items)
+
     def char_to_token(self, batch_or_char_index: int, char_index: Optional[int] = None):
         if char_index is None:
             return self._items[0].char_to_token(batch_or_char_index)
