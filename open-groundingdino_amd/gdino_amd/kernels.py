@@ -19,7 +19,6 @@ until its HIP kernel lands.  Tests may install oracle implementations through
 from __future__ import annotations
 
 import contextlib
-import math
 from typing import Callable, Dict, Optional
 
 import torch

@@ -3,8 +3,7 @@ groundingdino/util/misc.py and timm): NestedTensor, padding of image lists,
 inverse_sigmoid, distributed helpers, DropPath, trunc_normal_."""
 from __future__ import annotations
 
-import math
-from typing import List, Optional
+from typing import Optional
 
 import torch
 import torch.distributed as dist

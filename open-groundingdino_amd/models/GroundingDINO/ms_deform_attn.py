@@ -29,7 +29,6 @@ from typing import Optional
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 from torch.nn.init import constant_, xavier_uniform_
 
 from gdino_amd import castcache
