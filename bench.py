@@ -105,10 +105,18 @@ def cpu_baseline(bs):
             out.sum().backward()
         return time.perf_counter() - t0
 
-    t_enc_f = case(S, False)
-    t_enc_fb = case(S, True)
-    t_dec_fb = case(900, True)
-    per_step = 6 * t_enc_f + 6 * t_enc_fb + 6 * t_dec_fb
+    def per_step_time():
+        t = (case(S, False), case(S, True), case(900, True))
+        return t, 6 * sum(t)
+
+    (t_enc_f, t_enc_fb, t_dec_fb), per_step = per_step_time()
+    threads = torch.get_num_threads()
+    # also at one thread (the reference fallback's scalar rate)
+    torch.set_num_threads(1)
+    try:
+        (s_enc_f, s_enc_fb, s_dec_fb), per_step_1 = per_step_time()
+    finally:
+        torch.set_num_threads(threads)
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -121,8 +129,10 @@ def cpu_baseline(bs):
     return {
         "value": bs / per_step,
         "unit": "images/s (MSDA fwd+bwd share of the train step only)",
-        "cores": torch.get_num_threads(),
+        "cores": threads,
         "kind": "port",
+        "single_thread": {"value": bs / per_step_1, "cores": 1,
+                          "sample": f"same calls at 1 thread: {s_enc_f:.2f}s / {s_enc_fb:.2f}s / {s_dec_fb:.2f}s"},
         "sample": (f"reference pure-PyTorch MSDA fallback (grid_sample restatement, oracle/msda_torch.py) "
                    f"on {model}, os.cpu_count()={os.cpu_count()}: 1x encoder fwd {t_enc_f:.2f}s, "
                    f"1x encoder fwd+bwd {t_enc_fb:.2f}s, 1x decoder fwd+bwd {t_dec_fb:.2f}s at bs={bs} "

@@ -37,6 +37,8 @@ def test_bench_prints_the_contract_json_line(capsys):
     cb = res["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
     assert cb["unit"].startswith("images/s")
+    st = cb["single_thread"]
+    assert st["cores"] == 1 and 0 < st["value"]
 
 
 def _rank_worker(rank, world, port, q):
