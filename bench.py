@@ -140,6 +140,25 @@ def cpu_baseline(bs):
     }
 
 
+def pmc_traffic(kname, bs):
+    """HBM bytes per launch of the dominant MSDA kernel from the newest
+    profiles/*_pmc_traffic.json (tools/pmc_traffic.py over separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench), matched by
+    kernel and launch grid; None when no such profile is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    kind, lq = kname
+    units = bs * lq * 8  # N * Lq * M
+    grid = {"bwd": -(-units // 8) * 256, "fwd": -(-units // 64) * 256}[kind]  # threads (blocks x 256)
+    with open(files[-1]) as f:
+        for k in json.load(f)["kernels"]:
+            if f"msda_{kind}" in k["kernel"] and k["grid"] == grid and k["traffic_bytes"] is not None:
+                return k["traffic_bytes"]
+    return None
+
+
 def main(argv=None, device_type="cuda"):
     """device_type="cpu" exists for tests/test_bench_contract.py only (the
     HIP ops are then routed to the oracle by the test); the bench itself
@@ -215,7 +234,7 @@ def main(argv=None, device_type="cuda"):
         achieved = kd["bytes"] / avg_s
         roofline = {"bound": "hbm", "kernel": f"msda_{kname[0]} (Lq={kname[1]})",
                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK, "traffic": None,
+                    "frac": achieved / HBM_PEAK, "traffic": pmc_traffic(kname, a.bs),
                     "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"]}
     kernels = {f"msda_{k}_lq{lq}": {"launches": d["n"], "avg_us": d["ms"] / d["n"] * 1e3,
                                      "algo_bytes": d["bytes"], "GBps": d["bytes"] / (d["ms"] / d["n"] * 1e-3) / 1e9}
