@@ -27,7 +27,11 @@ core)
   T 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/s_pmc_fetch -o run -- \
       python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_fetch.log 2>&1 &&
   T 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/s_pmc_write -o run -- \
-      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_write.log 2>&1
+      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_write.log 2>&1 &&
+  # 7) host-only: per-launch bytes per (kernel, grid); copy the JSON to
+  # profiles/rNN_pmc_traffic.json so bench.py's roofline carries `traffic`
+  python3 tools/pmc_traffic.py --fetch gpurun_out/s_pmc_fetch --write gpurun_out/s_pmc_write \
+      --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
   ;;
 tune)
   # TunableOp: tune the step's GEMM shapes, then bench with the table
