@@ -25,188 +25,99 @@
 // pad_l[b, t] masks text column t out of every row softmax (P_v = 0).
 #include "gd_common.h"
 
+#include <algorithm>
+#include <initializer_list>
+#include <type_traits>
+
 namespace gd {
 namespace {
-
-constexpr int kRowsPerChunk = 128;
-
-template <typename T> __device__ __forceinline__ float ldf(const T* p);
-template <> __device__ __forceinline__ float ldf<float>(const float* p) { return *p; }
-template <> __device__ __forceinline__ float ldf<uint16_t>(const uint16_t* p) { return bf16_to_f32(*p); }
-template <typename T> __device__ __forceinline__ void stf(T* p, float v);
-template <> __device__ __forceinline__ void stf<float>(float* p, float v) { *p = v; }
-template <> __device__ __forceinline__ void stf<uint16_t>(uint16_t* p, float v) { *p = f32_to_bf16(v); }
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// grid (nchunk, BH), block 256: thread owns columns t = tid, tid+256, ...
-// and walks the chunk's rows (coalesced across the block).
-template <typename T>
-__global__ void __launch_bounds__(256)
-colstats_kernel(const T* __restrict__ s, const uint8_t* __restrict__ pad_v, int H, int S, int Tn,
-                float* __restrict__ pm, float* __restrict__ pl) {
-  const int chunk = blockIdx.x, bh = blockIdx.y, b = bh / H;
-  const int r0 = chunk * kRowsPerChunk;
-  const int r1 = min(S, r0 + kRowsPerChunk);
-  const size_t nchunk = gridDim.x;
-  for (int t = threadIdx.x; t < Tn; t += blockDim.x) {
-    float m = -INFINITY, l = 0.f;
-    for (int r = r0; r < r1; ++r) {
-      if (pad_v && pad_v[size_t(b) * S + r]) continue;
-      const float x = ldf<T>(s + (size_t(bh) * S + r) * Tn + t);
-      if (x > m) {
-        l = l * __expf(m - x) + 1.f;
-        m = x;
-      } else {
-        l += __expf(x - m);
-      }
-    }
-    pm[(size_t(bh) * nchunk + chunk) * Tn + t] = m;
-    pl[(size_t(bh) * nchunk + chunk) * Tn + t] = l;
-  }
-}
-
-// grid BH, block 256: merge nchunk partials of each column.
-__global__ void __launch_bounds__(256)
-colmerge_kernel(const float* __restrict__ pm, const float* __restrict__ pl, int nchunk, int Tn,
-                float* __restrict__ col_m, float* __restrict__ col_inv) {
-  const int bh = blockIdx.x;
-  for (int t = threadIdx.x; t < Tn; t += blockDim.x) {
-    float m = -INFINITY;
-    for (int c = 0; c < nchunk; ++c) m = fmaxf(m, pm[(size_t(bh) * nchunk + c) * Tn + t]);
-    float l = 0.f;
-    if (m != -INFINITY)
-      for (int c = 0; c < nchunk; ++c) {
-        const float mc = pm[(size_t(bh) * nchunk + c) * Tn + t];
-        if (mc != -INFINITY) l += pl[(size_t(bh) * nchunk + c) * Tn + t] * __expf(mc - m);
-      }
-    col_m[size_t(bh) * Tn + t] = m;
-    col_inv[size_t(bh) * Tn + t] = l > 0.f ? 1.f / l : 0.f;
-  }
-}
-
-// one wave per row of [BH*S, T]
-template <typename T>
-__global__ void __launch_bounds__(256)
-rows_fwd_kernel(const T* __restrict__ s, const uint8_t* __restrict__ pad_v, const uint8_t* __restrict__ pad_l,
-                const float* __restrict__ col_m, const float* __restrict__ col_inv, int H, int S, int Tn,
-                int64_t nrows, T* __restrict__ pv, T* __restrict__ plo) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (row >= nrows) return;
-  const int bh = int(row / S), r = int(row % S), b = bh / H;
-  const T* sr = s + row * Tn;
-  const bool row_pad = pad_v && pad_v[size_t(b) * S + r];
-  constexpr int MAXE = 16;  // T <= 1024
-  float x[MAXE];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < MAXE; ++j) {
-    const int t = lane + 64 * j;
-    x[j] = -INFINITY;
-    if (t < Tn) {
-      const float v = ldf<T>(sr + t);
-      const bool cp = pad_l && pad_l[size_t(b) * Tn + t];
-      x[j] = cp ? -INFINITY : v;
-      mx = fmaxf(mx, x[j]);
-      // column softmax output (independent of the row statistics)
-      const float ci = col_inv[size_t(bh) * Tn + t];
-      const float pcol = (row_pad || ci == 0.f) ? 0.f : __expf(v - col_m[size_t(bh) * Tn + t]) * ci;
-      stf<T>(plo + row * Tn + t, pcol);
-    }
-  }
-  mx = wave_max(mx);
-  float sum = 0.f;
-#pragma unroll
-  for (int j = 0; j < MAXE; ++j) {
-    const int t = lane + 64 * j;
-    if (t < Tn) {
-      x[j] = (mx == -INFINITY) ? 0.f : __expf(x[j] - mx);
-      sum += x[j];
-    }
-  }
-  sum = wave_sum(sum);
-  const float inv = sum > 0.f ? 1.f / sum : 0.f;
-#pragma unroll
-  for (int j = 0; j < MAXE; ++j) {
-    const int t = lane + 64 * j;
-    if (t < Tn) stf<T>(pv + row * Tn + t, x[j] * inv);
-  }
-}
-
-// backward: column partial sums of dP_l * P_l
-template <typename T>
-__global__ void __launch_bounds__(256)
-colsum_kernel(const T* __restrict__ plo, const T* __restrict__ dpl, int S, int Tn, float* __restrict__ part) {
-  const int chunk = blockIdx.x, bh = blockIdx.y;
-  const int r0 = chunk * kRowsPerChunk;
-  const int r1 = min(S, r0 + kRowsPerChunk);
-  const size_t nchunk = gridDim.x;
-  for (int t = threadIdx.x; t < Tn; t += blockDim.x) {
-    float acc = 0.f;
-    for (int r = r0; r < r1; ++r) {
-      const size_t o = (size_t(bh) * S + r) * Tn + t;
-      acc += ldf<T>(plo + o) * ldf<T>(dpl + o);
-    }
-    part[(size_t(bh) * nchunk + chunk) * Tn + t] = acc;
-  }
-}
-
-__global__ void __launch_bounds__(256)
-colsum_merge_kernel(const float* __restrict__ part, int nchunk, int Tn, float* __restrict__ csum) {
-  const int bh = blockIdx.x;
-  for (int t = threadIdx.x; t < Tn; t += blockDim.x) {
-    float acc = 0.f;
-    for (int c = 0; c < nchunk; ++c) acc += part[(size_t(bh) * nchunk + c) * Tn + t];
-    csum[size_t(bh) * Tn + t] = acc;
-  }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256)
-rows_bwd_kernel(const T* __restrict__ pv, const T* __restrict__ plo, const T* __restrict__ dpv,
-                const T* __restrict__ dpl, const float* __restrict__ csum, int S, int Tn, int64_t nrows,
-                T* __restrict__ ds) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (row >= nrows) return;
-  const int bh = int(row / S);
-  constexpr int MAXE = 16;
-  float p[MAXE], g[MAXE];
-  float r = 0.f;
-#pragma unroll
-  for (int j = 0; j < MAXE; ++j) {
-    const int t = lane + 64 * j;
-    p[j] = g[j] = 0.f;
-    if (t < Tn) {
-      p[j] = ldf<T>(pv + row * Tn + t);
-      g[j] = ldf<T>(dpv + row * Tn + t);
-      r += p[j] * g[j];
-    }
-  }
-  r = wave_sum(r);
-#pragma unroll
-  for (int j = 0; j < MAXE; ++j) {
-    const int t = lane + 64 * j;
-    if (t < Tn) {
-      const float q = ldf<T>(plo + row * Tn + t);
-      const float gq = ldf<T>(dpl + row * Tn + t);
-      const float v = p[j] * (g[j] - r) + q * (gq - csum[size_t(bh) * Tn + t]);
-      stf<T>(ds + row * Tn + t, v);
-    }
-  }
-}
+#include "biattn_kernels.inc"
 
 inline int nchunks(int S) { return (S + kRowsPerChunk - 1) / kRowsPerChunk; }
+
+inline bool aligned_to(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+// Slots per lane: smallest power of two E with 64*E >= T (T <= 1024).
+inline int slots_for(int Tn) {
+  int e = 1;
+  while (64 * e < Tn) e <<= 1;
+  return e;
+}
+
+// Contiguous slots need T == 64*E and every row operand aligned to its
+// E-element vector (capped at 16 B: wider slots are several dwordx4 loads).
+inline bool contig_ok(int Tn, size_t elem, std::initializer_list<const void*> ptrs) {
+  const int e = slots_for(Tn);
+  if (Tn != 64 * e) return false;
+  const size_t a = std::min<size_t>(16, size_t(e) * elem);
+  for (const void* p : ptrs)
+    if (!aligned_to(p, a)) return false;
+  return true;
+}
+
+// Calls fn(integral_constant<int, E>, bool_constant<CONTIG>) for the run-time
+// (slots_for(T), contig) pair.
+template <typename Fn>
+void with_slots(int Tn, bool contig, Fn&& fn) {
+  using std::integral_constant;
+  using std::true_type;
+  using std::false_type;
+  switch (slots_for(Tn)) {
+    case 1: contig ? fn(integral_constant<int, 1>{}, true_type{}) : fn(integral_constant<int, 1>{}, false_type{}); break;
+    case 2: contig ? fn(integral_constant<int, 2>{}, true_type{}) : fn(integral_constant<int, 2>{}, false_type{}); break;
+    case 4: contig ? fn(integral_constant<int, 4>{}, true_type{}) : fn(integral_constant<int, 4>{}, false_type{}); break;
+    case 8: contig ? fn(integral_constant<int, 8>{}, true_type{}) : fn(integral_constant<int, 8>{}, false_type{}); break;
+    default: contig ? fn(integral_constant<int, 16>{}, true_type{}) : fn(integral_constant<int, 16>{}, false_type{}); break;
+  }
+}
+
+template <typename T>
+gd_status softmax_fwd(const void* s, const uint8_t* pad_v, const uint8_t* pad_l, int B, int H, int S, int Tn,
+                      void* pv, void* pl, void* workspace, hipStream_t st) {
+  const int bh = B * H, nc = nchunks(S);
+  float* pm = static_cast<float*>(workspace);
+  float* plp = pm + size_t(bh) * nc * Tn;
+  float* col_m = plp + size_t(bh) * nc * Tn;
+  float* col_inv = col_m + size_t(bh) * Tn;
+  const int64_t nrows = int64_t(bh) * S;
+  const int rblocks = int((nrows + 3) / 4);
+  hipLaunchKernelGGL((colstats_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
+                     (const T*)s, pad_v, H, S, Tn, pm, plp);
+  GD_LAUNCH_CHECK("biattn colstats");
+  hipLaunchKernelGGL((colmerge_kernel), dim3((Tn + 63) / 64, bh), dim3(1024), 0, st,
+                     pm, plp, nc, Tn, col_m, col_inv);
+  GD_LAUNCH_CHECK("biattn colmerge");
+  const bool contig = contig_ok(Tn, sizeof(T), {s, pv, pl}) && aligned_to(col_m, 16) && aligned_to(col_inv, 16);
+  with_slots(Tn, contig, [&](auto e, auto c) {
+    hipLaunchKernelGGL((rows_fwd_kernel<T, decltype(e)::value, decltype(c)::value>), dim3(rblocks), dim3(256), 0, st,
+                     (const T*)s, pad_v, pad_l, col_m, col_inv, H, S, Tn, nrows, (T*)pv, (T*)pl);
+  });
+  GD_LAUNCH_CHECK("biattn rows_fwd");
+  return GD_OK;
+}
+
+template <typename T>
+gd_status softmax_bwd(const void* pv, const void* pl, const void* dpv, const void* dpl, int B, int H, int S, int Tn,
+                      void* ds, void* workspace, hipStream_t st) {
+  const int bh = B * H, nc = nchunks(S);
+  float* part = static_cast<float*>(workspace);
+  float* csum = part + size_t(bh) * nc * Tn * 2;
+  const int64_t nrows = int64_t(bh) * S;
+  const int rblocks = int((nrows + 3) / 4);
+  hipLaunchKernelGGL((colsum_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
+                     (const T*)pl, (const T*)dpl, S, Tn, part);
+  GD_LAUNCH_CHECK("biattn colsum");
+  hipLaunchKernelGGL((colsum_merge_kernel), dim3((Tn + 63) / 64, bh), dim3(1024), 0, st,
+                     part, nc, Tn, csum);
+  GD_LAUNCH_CHECK("biattn colsum_merge");
+  const bool contig = contig_ok(Tn, sizeof(T), {pv, pl, dpv, dpl, ds}) && aligned_to(csum, 16);
+  with_slots(Tn, contig, [&](auto e, auto c) {
+    hipLaunchKernelGGL((rows_bwd_kernel<T, decltype(e)::value, decltype(c)::value>), dim3(rblocks), dim3(256), 0, st,
+                     (const T*)pv, (const T*)pl, (const T*)dpv, (const T*)dpl, csum, S, Tn, nrows, (T*)ds);
+  });
+  GD_LAUNCH_CHECK("biattn rows_bwd");
+  return GD_OK;
+}
 
 }  // namespace
 }  // namespace gd
@@ -227,31 +138,8 @@ extern "C" gd_status gd_biattn_softmax_fwd(gd_dtype dt, const void* s, const uin
   if (B == 0 || S == 0) return GD_OK;
   GD_REQUIRE(s && pv && pl && workspace, "biattn_fwd: null pointer");
   hipStream_t st = as_hip(stream);
-  const int bh = B * H, nc = nchunks(S);
-  float* pm = static_cast<float*>(workspace);
-  float* plp = pm + size_t(bh) * nc * T;
-  float* col_m = plp + size_t(bh) * nc * T;
-  float* col_inv = col_m + size_t(bh) * T;
-  const int64_t nrows = int64_t(bh) * S;
-  const int rblocks = int((nrows + 3) / 4);
-  if (dt == GD_BF16) {
-    colstats_kernel<uint16_t><<<dim3(nc, bh), 256, 0, st>>>((const uint16_t*)s, pad_v, H, S, T, pm, plp);
-    GD_LAUNCH_CHECK("biattn colstats");
-    colmerge_kernel<<<bh, 256, 0, st>>>(pm, plp, nc, T, col_m, col_inv);
-    GD_LAUNCH_CHECK("biattn colmerge");
-    rows_fwd_kernel<uint16_t><<<rblocks, 256, 0, st>>>((const uint16_t*)s, pad_v, pad_l, col_m, col_inv, H, S,
-                                                      T, nrows, (uint16_t*)pv, (uint16_t*)pl);
-    GD_LAUNCH_CHECK("biattn rows_fwd");
-  } else {
-    colstats_kernel<float><<<dim3(nc, bh), 256, 0, st>>>((const float*)s, pad_v, H, S, T, pm, plp);
-    GD_LAUNCH_CHECK("biattn colstats");
-    colmerge_kernel<<<bh, 256, 0, st>>>(pm, plp, nc, T, col_m, col_inv);
-    GD_LAUNCH_CHECK("biattn colmerge");
-    rows_fwd_kernel<float><<<rblocks, 256, 0, st>>>((const float*)s, pad_v, pad_l, col_m, col_inv, H, S, T,
-                                                   nrows, (float*)pv, (float*)pl);
-    GD_LAUNCH_CHECK("biattn rows_fwd");
-  }
-  return GD_OK;
+  return dt == GD_BF16 ? softmax_fwd<uint16_t>(s, pad_v, pad_l, B, H, S, T, pv, pl, workspace, st)
+                       : softmax_fwd<float>(s, pad_v, pad_l, B, H, S, T, pv, pl, workspace, st);
 }
 
 extern "C" gd_status gd_biattn_softmax_bwd(gd_dtype dt, const void* pv, const void* pl, const void* dpv,
@@ -263,28 +151,6 @@ extern "C" gd_status gd_biattn_softmax_bwd(gd_dtype dt, const void* pv, const vo
   if (B == 0 || S == 0) return GD_OK;
   GD_REQUIRE(pv && pl && dpv && dpl && ds && workspace, "biattn_bwd: null pointer");
   hipStream_t st = as_hip(stream);
-  const int bh = B * H, nc = nchunks(S);
-  float* part = static_cast<float*>(workspace);
-  float* csum = part + size_t(bh) * nc * T * 2;
-  const int64_t nrows = int64_t(bh) * S;
-  const int rblocks = int((nrows + 3) / 4);
-  if (dt == GD_BF16) {
-    colsum_kernel<uint16_t><<<dim3(nc, bh), 256, 0, st>>>((const uint16_t*)pl, (const uint16_t*)dpl, S, T, part);
-    GD_LAUNCH_CHECK("biattn colsum");
-    colsum_merge_kernel<<<bh, 256, 0, st>>>(part, nc, T, csum);
-    GD_LAUNCH_CHECK("biattn colsum_merge");
-    rows_bwd_kernel<uint16_t><<<rblocks, 256, 0, st>>>((const uint16_t*)pv, (const uint16_t*)pl,
-                                                      (const uint16_t*)dpv, (const uint16_t*)dpl, csum, S, T,
-                                                      nrows, (uint16_t*)ds);
-    GD_LAUNCH_CHECK("biattn rows_bwd");
-  } else {
-    colsum_kernel<float><<<dim3(nc, bh), 256, 0, st>>>((const float*)pl, (const float*)dpl, S, T, part);
-    GD_LAUNCH_CHECK("biattn colsum");
-    colsum_merge_kernel<<<bh, 256, 0, st>>>(part, nc, T, csum);
-    GD_LAUNCH_CHECK("biattn colsum_merge");
-    rows_bwd_kernel<float><<<rblocks, 256, 0, st>>>((const float*)pv, (const float*)pl, (const float*)dpv,
-                                                   (const float*)dpl, csum, S, T, nrows, (float*)ds);
-    GD_LAUNCH_CHECK("biattn rows_bwd");
-  }
-  return GD_OK;
+  return dt == GD_BF16 ? softmax_bwd<uint16_t>(pv, pl, dpv, dpl, B, H, S, T, ds, workspace, st)
+                       : softmax_bwd<float>(pv, pl, dpv, dpl, B, H, S, T, ds, workspace, st);
 }

@@ -1,0 +1,228 @@
+// Host-side SIMT emulation of the HIP subset the gd kernels use.
+//
+// TEST INFRASTRUCTURE ONLY (tests/emu): the product's own csrc/*.hip files are
+// compiled by the host clang++ against this header (it shadows
+// <hip/hip_runtime.h> through -I), giving tests/emu/_build/libgd_emu.so with the
+// same C ABI as libgdino_amd.so, operating on host pointers.  Tests use it to
+// run the exact kernel sources -- indexing, LDS use, barriers, cross-lane
+// exchanges, launch geometry -- on the CPU when no GPU is available, against
+// the oracle.  It is never loaded by the product (gdino_amd._lib loads only
+// the gfx950 library) and it says nothing about speed.
+//
+// Model: one workgroup at a time; each work-item is a ucontext fiber on one OS
+// thread, scheduled round-robin.  A fiber runs until it has to wait:
+//   * __syncthreads(): until every live work-item of the block has arrived;
+//   * cross-lane reads (__shfl_xor, ds_swizzle, DPP): until the source lane
+//     has published its value for the same exchange (each lane publishes into
+//     an append-only log indexed by its exchange count, so a source never
+//     overwrites a value a slower reader still needs).
+// Wave = 64 consecutive work-items.  LDS (__shared__) is a static array,
+// zero-initialised once, like uninitialised LDS it must be written before use.
+// Global float atomics are plain read-modify-writes (one OS thread).
+#pragma once
+
+#include <ucontext.h>
+
+#include <climits>
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+
+struct dim3 {
+  unsigned x, y, z;
+  constexpr dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+struct float2 { float x, y; };
+struct float4 { float x, y, z, w; };
+struct uint2 { unsigned x, y; };
+struct uint4 { unsigned x, y, z, w; };
+inline float2 make_float2(float a, float b) { return {a, b}; }
+inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
+inline uint2 make_uint2(unsigned a, unsigned b) { return {a, b}; }
+
+typedef int hipError_t;
+constexpr hipError_t hipSuccess = 0;
+typedef struct ihipStream_t* hipStream_t;
+#define HIP_VERSION 0
+
+struct hipDeviceProp_t {
+  char gcnArchName[256];
+};
+inline const char* hipGetErrorString(hipError_t) { return "emulated HIP error"; }
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
+  memset(p, v, n);
+  return hipSuccess;
+}
+inline hipError_t hipRuntimeGetVersion(int* v) {
+  *v = 0;
+  return hipSuccess;
+}
+inline hipError_t hipGetDevice(int* d) {
+  *d = 0;
+  return hipSuccess;
+}
+inline hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int) {
+  snprintf(p->gcnArchName, sizeof(p->gcnArchName), "host-emulator");
+  return hipSuccess;
+}
+
+inline float __int_as_float(int v) { float f; memcpy(&f, &v, 4); return f; }
+inline int __float_as_int(float f) { int v; memcpy(&v, &f, 4); return v; }
+inline float __uint_as_float(unsigned v) { float f; memcpy(&f, &v, 4); return f; }
+inline unsigned __float_as_uint(float f) { unsigned v; memcpy(&v, &f, 4); return v; }
+inline float __expf(float x) { return expf(x); }
+inline int min(int a, int b) { return a < b ? a : b; }
+inline int max(int a, int b) { return a > b ? a : b; }
+
+namespace gd_emu {
+
+struct Item {
+  ucontext_t ctx;
+  std::vector<char> stack;
+  dim3 tid;
+  bool done = false;
+  bool at_barrier = false;
+  unsigned barrier_gen = 0;
+  size_t nxchg = 0;                  // cross-lane exchanges performed
+  std::vector<uint64_t> published;   // value published at each exchange
+};
+
+struct Grid {
+  dim3 grid, block, bid;
+  std::vector<Item> items;
+  size_t cur = 0;
+  unsigned live = 0, arrived = 0, gen = 0;
+  ucontext_t sched;
+  void (*body)(void*) = nullptr;
+  void* body_arg = nullptr;
+};
+
+Grid& grid();  // defined in gd_emu.cpp
+void note_progress();
+void yield();  // back to the scheduler
+void run(dim3 g, dim3 b, void (*body)(void*), void* arg);
+
+inline Item& self() { return grid().items[grid().cur]; }
+inline unsigned flat_id() { return unsigned(grid().cur); }
+
+// Publish `bits` as this lane's value for its next exchange; return the value
+// lane `src` (flat work-item index) published for the same exchange.
+inline uint64_t exchange(uint64_t bits, unsigned src) {
+  Grid& g = grid();
+  Item& me = g.items[g.cur];
+  const size_t k = me.nxchg++;
+  me.published.push_back(bits);
+  note_progress();
+  if (src >= g.items.size()) {
+    fprintf(stderr, "gd_emu: lane exchange with work-item %u outside the block\n", src);
+    abort();
+  }
+  for (;;) {
+    Item& o = g.items[src];
+    if (o.published.size() > k) return o.published[k];
+    if (o.done) {
+      fprintf(stderr, "gd_emu: work-item %u reads exited work-item %u (exchange %zu)\n", flat_id(), src, k);
+      abort();
+    }
+    yield();
+  }
+}
+
+template <typename V>
+inline V xchg_from(V v, unsigned src) {
+  static_assert(sizeof(V) <= 8, "exchange of at most 64 bits");
+  uint64_t b = 0;
+  memcpy(&b, &v, sizeof(V));
+  const uint64_t r = exchange(b, src);
+  V out;
+  memcpy(&out, &r, sizeof(V));
+  return out;
+}
+
+inline unsigned wave_base() { return flat_id() & ~63u; }
+inline unsigned lane_id() { return flat_id() & 63u; }
+
+// ds_swizzle, bitmask mode (offset bit 15 = 0) inside 32-lane groups
+inline int ds_swizzle(int v, int pattern) {
+  if (pattern & 0x8000) {
+    fprintf(stderr, "gd_emu: ds_swizzle QDMode pattern 0x%x not emulated\n", pattern);
+    abort();
+  }
+  const unsigned and_m = pattern & 0x1F, or_m = (pattern >> 5) & 0x1F, xor_m = (pattern >> 10) & 0x1F;
+  const unsigned lane = lane_id();
+  const unsigned src = (lane & ~31u) | ((((lane & 31u) & and_m) | or_m) ^ xor_m);
+  return xchg_from(v, wave_base() + src);
+}
+
+// DPP (row_mask = bank_mask = 0xF): quad_perm, row_half_mirror, row_ror
+template <typename V>
+inline V update_dpp(V old, V src, int ctrl, int row_mask, int bank_mask, bool) {
+  if (row_mask != 0xF || bank_mask != 0xF) {
+    fprintf(stderr, "gd_emu: DPP with partial masks not emulated\n");
+    abort();
+  }
+  (void)old;
+  const unsigned lane = lane_id();
+  unsigned from;
+  if (ctrl >= 0 && ctrl <= 0xFF) {  // quad_perm
+    from = (lane & ~3u) | ((unsigned(ctrl) >> (2 * (lane & 3u))) & 3u);
+  } else if (ctrl == 0x141) {  // row_half_mirror
+    from = (lane & ~7u) | (7u - (lane & 7u));
+  } else if (ctrl >= 0x121 && ctrl <= 0x12F) {  // row_ror:n
+    const unsigned n = unsigned(ctrl) & 0xF;
+    from = (lane & ~15u) | (((lane & 15u) + n) & 15u);
+  } else {
+    fprintf(stderr, "gd_emu: DPP control 0x%x not emulated\n", ctrl);
+    abort();
+  }
+  return xchg_from(src, wave_base() + from);
+}
+
+template <typename V>
+inline V shfl_xor(V v, int mask, int width) {
+  const unsigned lane = lane_id();
+  const unsigned w = unsigned(width);
+  const unsigned src = (lane & ~(w - 1)) | (((lane & (w - 1)) ^ unsigned(mask)) & (w - 1));
+  return xchg_from(v, wave_base() + src);
+}
+
+void syncthreads();
+
+template <typename F>
+void launch(dim3 g, dim3 b, F&& f) {
+  auto thunk = [](void* p) { (*static_cast<F*>(p))(); };
+  run(g, b, thunk, &f);
+}
+
+}  // namespace gd_emu
+
+#define threadIdx (::gd_emu::self().tid)
+#define blockIdx (::gd_emu::grid().bid)
+#define gridDim (::gd_emu::grid().grid)
+#define blockDim (::gd_emu::grid().block)
+#define __syncthreads() ::gd_emu::syncthreads()
+#define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
+#define __builtin_amdgcn_ds_swizzle(v, pattern) ::gd_emu::ds_swizzle((v), (pattern))
+#define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) \
+  ::gd_emu::update_dpp((old), (src), (ctrl), (rm), (bm), (bc))
+#define hipLaunchKernelGGL(kernel, g, b, shm, stream, ...) \
+  ((void)(shm), (void)(stream), ::gd_emu::launch(dim3(g), dim3(b), [&]() { kernel(__VA_ARGS__); }))
+
+template <typename T>
+inline T atomicAdd(T* p, T v) {
+  const T old = *p;
+  *p = old + v;
+  return old;
+}

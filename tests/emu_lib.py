@@ -1,0 +1,108 @@
+"""ctypes front-end of the host-side SIMT emulator (tests/emu): the product's
+csrc/*.hip compiled as host C++ against tests/emu/include/hip/hip_runtime.h,
+exporting the same C ABI as libgdino_amd.so (include/gdino_amd.h) on host
+pointers.  Test infrastructure only: it lets the CPU suite execute the exact
+kernel sources (indexing, LDS, barriers, DPP/swizzle exchanges, launch
+geometry) against the oracle when no GPU is available."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EMU_DIR = os.path.join(ROOT, "tests", "emu")
+_LIB = None
+
+F32, F64, BF16 = 0, 1, 2
+_p, _i = ctypes.c_void_p, ctypes.c_int
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        # GD_EMU_ASAN=1: the AddressSanitizer build (the process must preload
+        # the clang ASan runtime; see tests/test_emu_kernels.py)
+        asan = os.environ.get("GD_EMU_ASAN") == "1"
+        subprocess.run(["make", "-s", "-C", EMU_DIR] + (["asan"] if asan else []), check=True)
+        _LIB = ctypes.CDLL(os.path.join(EMU_DIR, "_build", "libgd_emu_asan.so" if asan else "libgd_emu.so"))
+        _LIB.gd_msda_forward.argtypes = [_i, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p]
+        _LIB.gd_msda_backward.argtypes = [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p, _p, _p]
+        _LIB.gd_biattn_workspace_bytes.argtypes = [_i] * 4
+        _LIB.gd_biattn_workspace_bytes.restype = ctypes.c_size_t
+        _LIB.gd_biattn_softmax_fwd.argtypes = [_i, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]
+        _LIB.gd_biattn_softmax_bwd.argtypes = [_i, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]
+        _LIB.gd_last_error.restype = ctypes.c_char_p
+        _LIB.gd_runtime_info.restype = ctypes.c_char_p
+    return _LIB
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(lib().gd_last_error().decode())
+
+
+def _code(t):
+    return {torch.float32: F32, torch.float64: F64, torch.bfloat16: BF16}[t.dtype]
+
+
+def msda_forward(value, shapes, lsi, loc, attn):
+    """value [N,S,M,D] (f32/f64/bf16), loc/attn f32 (f64 for f64 value) -> out [N,Lq,M*D]."""
+    N, S, M, D = value.shape
+    _, Lq, _, L, P, _ = loc.shape
+    value, loc, attn = value.contiguous(), loc.contiguous(), attn.contiguous()
+    shapes, lsi = shapes.to(torch.int64).contiguous(), lsi.to(torch.int64).contiguous()
+    out = torch.empty(N, Lq, M * D, dtype=value.dtype)
+    _check(lib().gd_msda_forward(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc), _ptr(attn),
+                                 N, S, M, D, L, Lq, P, _ptr(out), None))
+    return out
+
+
+def msda_backward(value, shapes, lsi, loc, attn, grad_out):
+    """-> grad_value (f32, or f64 for f64 value), grad_loc, grad_attn."""
+    N, S, M, D = value.shape
+    _, Lq, _, L, P, _ = loc.shape
+    acc = torch.float64 if value.dtype == torch.float64 else torch.float32
+    value, loc, attn, grad_out = (t.contiguous() for t in (value, loc, attn, grad_out))
+    shapes, lsi = shapes.to(torch.int64).contiguous(), lsi.to(torch.int64).contiguous()
+    gv = torch.empty(N, S, M, D, dtype=acc)
+    gl = torch.empty(N, Lq, M, L, P, 2, dtype=acc)
+    ga = torch.empty(N, Lq, M, L, P, dtype=acc)
+    _check(lib().gd_msda_backward(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc), _ptr(attn),
+                                  _ptr(grad_out), N, S, M, D, L, Lq, P, _ptr(gv), _ptr(gl), _ptr(ga), None))
+    return gv, gl, ga
+
+
+def _u8(m):
+    return None if m is None else m.to(torch.uint8).contiguous()
+
+
+def biattn_softmax_fwd(s, pad_v=None, pad_l=None):
+    B, H, S, T = s.shape
+    s = s.contiguous()
+    pv, pl = torch.empty_like(s), torch.empty_like(s)
+    ws = torch.empty((int(lib().gd_biattn_workspace_bytes(B, H, S, T)) + 3) // 4, dtype=torch.float32)
+    mv, ml = _u8(pad_v), _u8(pad_l)
+    _check(lib().gd_biattn_softmax_fwd(_code(s), _ptr(s), _ptr(mv), _ptr(ml), B, H, S, T, _ptr(pv), _ptr(pl),
+                                       _ptr(ws), None))
+    return pv, pl
+
+
+def biattn_softmax_bwd(pv, pl, dpv, dpl):
+    B, H, S, T = pv.shape
+    pv, pl, dpv, dpl = (t.contiguous() for t in (pv, pl, dpv, dpl))
+    ds = torch.empty_like(pv)
+    ws = torch.empty((int(lib().gd_biattn_workspace_bytes(B, H, S, T)) + 3) // 4, dtype=torch.float32)
+    _check(lib().gd_biattn_softmax_bwd(_code(pv), _ptr(pv), _ptr(pl), _ptr(dpv), _ptr(dpl), B, H, S, T, _ptr(ds),
+                                       _ptr(ws), None))
+    return ds
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))

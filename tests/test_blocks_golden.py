@@ -28,6 +28,8 @@ def test_block_matches_reference_fp64(name):
     with oracle_msda():
         errs = compare(name, "cpu", torch.float64, tol=1e-9)
     assert errs
+    if name == "transformer":  # the encoder half is fp64 end to end
+        assert errs["hs_enc"] < 1e-9
 
 
 @pytest.mark.parametrize("name", ["biattn", "transformer"])
@@ -85,4 +87,4 @@ def test_full_model_matches_reference_fp64():
     small random BERT on both sides (block_spec.TINY_BERT)."""
     with oracle_msda():
         errs = compare("model", "cpu", torch.float64, tol=1e-9)
-    assert errs["pred_logits"] < 1e-9
+    assert errs["pred_logits"] < 1e-7  # block_harness.FP32_SEEDED

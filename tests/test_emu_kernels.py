@@ -1,0 +1,187 @@
+"""The HIP kernels' own sources, executed on the CPU by the host-side SIMT
+emulator (tests/emu, test infrastructure), against the oracle.
+
+Why: when no GPU is reachable, this is how kernel changes are checked before
+they ship -- the exact csrc/*.hip code with its indexing, LDS accumulator,
+barriers, DPP / ds_swizzle butterflies and launch geometry.  It does not
+replace the GPU parity tests (tests/test_msda_gpu.py, test_kernels_gpu.py),
+which run the gfx950 build on the box.
+
+The emulator itself is pinned by the kernels that passed the GPU tests in
+round 1 (msda_fwd_vec, msda_bwd_lane32): they must match the oracle here too.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import emu_lib as E
+import oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _levels_inputs(levels, n, lq, seed, vdtype=torch.float32, local=False, spread_px=2.0, outlier_frac=0.0):
+    shapes = torch.as_tensor(levels, dtype=torch.long)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S = int(shapes.prod(1).sum())
+    M, D, L, P = 8, 32, len(levels), 4
+    g = torch.Generator().manual_seed(seed)
+    if local:  # encoder: Lq == S, points near each query's own position
+        assert lq == S
+        refs = []
+        for (h, w) in levels:
+            yy, xx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+            refs.append(torch.stack([(xx.reshape(-1) + 0.5) / w, (yy.reshape(-1) + 0.5) / h], -1))
+        ref = torch.cat(refs).double()
+        wh = torch.as_tensor([(w, h) for (h, w) in levels], dtype=torch.float64)
+        off = torch.randn(n, S, M, L, P, 2, generator=g, dtype=torch.float64) * spread_px
+        loc = ref[None, :, None, None, None, :] + off / wh[None, None, None, :, None, :]
+        if outlier_frac:
+            pick = torch.rand(n, S, M, L, P, 1, generator=g) < outlier_frac
+            loc = torch.where(pick, torch.rand(loc.shape, generator=g, dtype=torch.float64) * 1.2 - 0.1, loc)
+        loc = loc.float()
+    else:
+        loc = torch.rand(n, lq, M, L, P, 2, generator=g) * 1.1 - 0.05
+    value = torch.randn(n, S, M, D, generator=g).to(vdtype)
+    attn = torch.rand(n, lq, M, L, P, generator=g) + 1e-5
+    attn = attn / attn.sum((-1, -2), keepdim=True)
+    grad_out = torch.randn(n, lq, M * D, generator=g).to(vdtype)
+    return value, shapes, lsi, loc, attn, grad_out
+
+
+def _oracle_bwd(value, shapes, lsi, loc, attn, grad_out):
+    return oracle.msda_backward(value.double().numpy(), shapes, lsi, loc.double(), attn.double(),
+                                grad_out.double().numpy())
+
+
+def _check_bwd(inputs, tol):
+    gv, gl, ga = E.msda_backward(*inputs)
+    rgv, rgl, rga = _oracle_bwd(*inputs)
+    assert E.rel_err(gv, rgv) < tol
+    assert E.rel_err(gl, rgl) < tol
+    assert E.rel_err(ga, rga) < tol
+    return gv, gl, ga
+
+
+SMALL = [(6, 9), (3, 5), (2, 3), (1, 2)]               # S = 76
+MEDIUM = [(13, 21), (7, 11), (4, 6), (2, 3)]           # S = 380 (tail tiles, tiles across levels)
+WIDE = [(20, 67), (10, 34), (5, 17), (3, 9)]           # level-0 boxes of 32-query tiles overflow LDS
+
+
+# ------------------------------------------------- emulator pinned by round-1
+@pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-5)])
+def test_emulated_verified_kernels_match_oracle(vdtype, tol):
+    """msda_fwd_vec / msda_bwd_lane32 passed the GPU parity tests in round 1;
+    the emulator must reproduce them (inputs are bf16-exact, so the oracle on
+    the same values is tight)."""
+    value, shapes, lsi, loc, attn, grad_out = _levels_inputs(MEDIUM, 2, 50, seed=1, vdtype=vdtype)
+    out = E.msda_forward(value, shapes, lsi, loc, attn)
+    ref = oracle.msda_forward(value.double().numpy(), shapes, lsi, loc.double(), attn.double())
+    assert E.rel_err(out.double(), ref) < (1e-5 if vdtype == torch.float32 else 1e-2)
+    _check_bwd((value, shapes, lsi, loc, attn, grad_out), tol)
+
+
+# ------------------------------------------- tiled (LDS) encoder backward
+@pytest.mark.parametrize("levels,n,local,outliers", [
+    (SMALL, 1, False, 0.0),     # every level box fits: all-LDS path
+    (MEDIUM, 2, True, 0.0),     # encoder geometry, batch boundary inside the grid
+    (MEDIUM, 2, True, 0.1),     # + outliers: mixed LDS / global atomics
+    (MEDIUM, 1, False, 0.0),    # uniform points: boxes overflow, global fallback
+    (WIDE, 1, True, 0.02),
+])
+def test_emulated_tiled_backward_matches_oracle(levels, n, local, outliers):
+    S = sum(h * w for h, w in levels)
+    inputs = _levels_inputs(levels, n, S, seed=S + n, local=local, outlier_frac=outliers)
+    _check_bwd(inputs, 1e-5)
+
+
+def test_emulated_tiled_backward_bf16():
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=5, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
+    _check_bwd(inputs, 1e-5)  # bf16-exact inputs, fp32 accumulation
+
+
+def test_emulated_tiled_equals_direct_atomic_kernel(monkeypatch):
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=9, local=True, outlier_frac=0.05)
+    tiled = E.msda_backward(*inputs)
+    monkeypatch.setenv("GD_MSDA_BWD", "lane32")
+    direct = E.msda_backward(*inputs)
+    torch.testing.assert_close(tiled[0], direct[0], rtol=1e-5, atol=1e-6)
+    assert torch.equal(tiled[1], direct[1]) and torch.equal(tiled[2], direct[2])
+
+
+# --------------------------------------------------- BiAttention softmax
+def _softmax_ref(s, pad_v, pad_l):
+    s = s.double()
+    pv = torch.softmax(s.masked_fill(pad_l[:, None, None, :], float("-inf")), -1).nan_to_num(0.0)
+    pl = torch.softmax(s.masked_fill(pad_v[:, None, :, None], float("-inf")), -2).nan_to_num(0.0)
+    return pv, pl
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("shape", [(2, 2, 300, 40), (1, 2, 200, 100), (1, 1, 333, 64), (2, 1, 260, 128),
+                                   (1, 1, 130, 256), (1, 1, 70, 600)])
+def test_emulated_biattn_softmax(dtype, tol, shape):
+    b, h, s_len, t = shape
+    g = torch.Generator().manual_seed(sum(shape))
+    s = (torch.randn(b, h, s_len, t, generator=g) * 2).to(dtype)
+    pad_v = torch.zeros(b, s_len, dtype=torch.bool)
+    pad_l = torch.zeros(b, t, dtype=torch.bool)
+    pad_v[-1, s_len * 3 // 4:] = True
+    pad_l[0, t // 2:] = True
+    pv, pl = E.biattn_softmax_fwd(s, pad_v, pad_l)
+    sd = s.double().requires_grad_(True)
+    rpv, rpl = _softmax_ref(sd, pad_v, pad_l)
+    assert E.rel_err(pv.double(), rpv.detach()) < tol
+    assert E.rel_err(pl.double(), rpl.detach()) < tol
+    dpv = torch.randn(pv.shape, generator=g).to(dtype)
+    dpl = torch.randn(pl.shape, generator=g).to(dtype)
+    ds = E.biattn_softmax_bwd(pv, pl, dpv, dpl)
+    # the kernel's backward uses its own P_v / P_l: compare with the exact
+    # Jacobian products evaluated at those probabilities
+    pvd, pld = pv.double(), pl.double()
+    r = (dpv.double() * pvd).sum(-1, keepdim=True)
+    c = (dpl.double() * pld).sum(-2, keepdim=True)
+    ref = pvd * (dpv.double() - r) + pld * (dpl.double() - c)
+    assert E.rel_err(ds.double(), ref) < tol
+    # and with autograd of the reference softmaxes
+    ((rpv * dpv.double()).sum() + (rpl * dpl.double()).sum()).backward()
+    assert E.rel_err(ds.double(), sd.grad) < (1e-5 if dtype == torch.float32 else 3e-2)
+
+
+# ------------------------------------------------------ AddressSanitizer
+_ASAN_SCRIPT = r"""
+import sys
+sys.path[:0] = {paths!r}
+import torch
+import test_emu_kernels as t
+S = sum(h * w for h, w in t.MEDIUM)
+t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=3, local=True, outlier_frac=0.1), 1e-5)
+t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)
+t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 37, seed=6), 1e-5)
+t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 2, 200, 100))
+t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
+print("asan-clean")
+"""
+
+
+def test_emulated_kernels_under_address_sanitizer():
+    """Out-of-bounds global or LDS accesses of the kernels (the usual cause
+    of a GPU memory fault) abort the ASan build of the emulator."""
+    clang = "/opt/rocm/lib/llvm/bin/clang++"
+    if not os.path.exists(clang):
+        pytest.skip("host clang++ not available")
+    rt = subprocess.run([clang, "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True,
+                        text=True).stdout.strip()
+    if not os.path.exists(rt):
+        pytest.skip("clang ASan runtime not available")
+    paths = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "open-groundingdino_amd")]
+    env = dict(os.environ, GD_EMU_ASAN="1", LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([sys.executable, "-c", _ASAN_SCRIPT.format(paths=paths)], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0 and "asan-clean" in r.stdout, r.stderr[-4000:]

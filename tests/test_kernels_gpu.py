@@ -30,7 +30,10 @@ def _bi_inputs(b, h, s, t, hd, dtype, seed=0, pad=True):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("shape", [(2, 4, 300, 40, 64), (1, 2, 1000, 256, 32), (2, 4, 2048, 256, 256)])
+# T = 40 / 100: strided lane slots (T not a multiple of 64); T = 64 / 128 / 256:
+# contiguous vector slots (E = 1 / 2 / 4 elements per lane)
+@pytest.mark.parametrize("shape", [(2, 4, 300, 40, 64), (1, 2, 700, 100, 32), (1, 2, 333, 64, 16),
+                                   (2, 2, 500, 128, 32), (1, 2, 1000, 256, 32), (2, 4, 2048, 256, 256)])
 def test_bi_attention_fwd_bwd(dtype, tol, shape):
     from gdino_amd.biattn import bi_attention_hip
     b, h, s, t, hd = shape

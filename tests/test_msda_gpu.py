@@ -180,6 +180,79 @@ def test_800x1333_shapes(lq, vdtype, tol):
     assert _rel_err(gl.cpu(), ref_gl) < tol
 
 
+# ------------------------------- encoder self-attention: tiled LDS backward
+def _encoder_inputs(levels, n, seed, vdtype, spread_px=2.0, outlier_frac=0.0):
+    """Lq == S (every value position is a query, in value order): points
+    within ~spread_px pixels of each query's own position on every level, as
+    the encoder samples (transformer.py:471-485 reference points + offsets);
+    outlier_frac of the points are redrawn uniformly (boxes too large for the
+    LDS accumulator -> the kernel's global-atomic fallback)."""
+    shapes = torch.as_tensor(levels, dtype=torch.long)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S = int(shapes.prod(1).sum())
+    M, D, L, P = 8, 32, len(levels), 4
+    g = torch.Generator().manual_seed(seed)
+    refs = []
+    for (h, w) in levels:
+        yy, xx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+        refs.append(torch.stack([(xx.reshape(-1) + 0.5) / w, (yy.reshape(-1) + 0.5) / h], -1))
+    ref = torch.cat(refs).double()  # [S, 2]
+    wh = torch.as_tensor([(w, h) for (h, w) in levels], dtype=torch.float64)
+    off = torch.randn(n, S, M, L, P, 2, generator=g, dtype=torch.float64) * spread_px / wh[None, None, None, :, None, :]
+    loc = ref[None, :, None, None, None, :] + off
+    if outlier_frac > 0:
+        pick = torch.rand(n, S, M, L, P, 1, generator=g) < outlier_frac
+        loc = torch.where(pick, torch.rand(loc.shape, generator=g, dtype=torch.float64) * 1.2 - 0.1, loc)
+    value = torch.randn(n, S, M, D, generator=g)
+    attn = torch.rand(n, S, M, L, P, generator=g) + 1e-5
+    attn = attn / attn.sum((-1, -2), keepdim=True)
+    grad_out = torch.randn(n, S, M * D, generator=g)
+    return (value.to(vdtype), shapes, lsi, loc.float(), attn.float(), grad_out.to(vdtype))
+
+
+def _check_bwd_vs_oracle(inputs, tol):
+    value, shapes, lsi, loc, attn, grad_out = inputs
+    dev = [t.to(DEV) for t in inputs]
+    gv, gl, ga = _msda().ms_deform_attn_backward(*dev, 64, grad_value_dtype=torch.float32)
+    torch.cuda.synchronize()
+    v = value.double().numpy()
+    ref_gv, ref_gl, ref_ga = oracle.msda_backward(v, shapes, lsi, loc.double(), attn.double(),
+                                                  grad_out.double().numpy())
+    assert _rel_err(gv.cpu(), ref_gv) < tol
+    assert _rel_err(ga.cpu(), ref_ga) < tol
+    assert _rel_err(gl.cpu(), ref_gl) < tol
+    return gv, gl, ga
+
+
+@pytest.mark.parametrize("levels,n", [([(6, 9), (3, 5), (2, 3), (1, 2)], 1),     # S=76: tiles cross levels
+                                      ([(13, 21), (7, 11), (4, 6), (2, 3)], 2),  # tail tile, n boundary
+                                      ([(40, 67), (20, 34), (10, 17), (5, 9)], 2)])
+@pytest.mark.parametrize("outliers", [0.0, 0.05])
+def test_encoder_tiled_backward_small(levels, n, outliers):
+    _check_bwd_vs_oracle(_encoder_inputs(levels, n, seed=len(levels) + n, vdtype=torch.float32,
+                                         outlier_frac=outliers), 1e-3)
+
+
+@pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+def test_encoder_tiled_backward_800x1333(vdtype, tol):
+    _check_bwd_vs_oracle(_encoder_inputs(LEVELS_800, 2, seed=7, vdtype=vdtype, outlier_frac=0.01), tol)
+
+
+def test_encoder_tiled_matches_direct_atomic_kernel(monkeypatch):
+    """Same sums, different order: the LDS-aggregated kernel against the
+    round-1 direct-atomic kernel (GD_MSDA_BWD=lane32) on one input."""
+    inputs = [t.to(DEV) for t in _encoder_inputs(LEVELS_800, 2, seed=11, vdtype=torch.float32)]
+    tiled = _msda().ms_deform_attn_backward(*inputs, 64)
+    monkeypatch.setenv("GD_MSDA_BWD", "lane32")
+    direct = _msda().ms_deform_attn_backward(*inputs, 64)
+    for a, b in zip(tiled, direct):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    # grad_loc / grad_attn do not involve atomics: same arithmetic (up to the
+    # compiler's FMA contraction choices in the two kernels)
+    torch.testing.assert_close(tiled[1], direct[1], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(tiled[2], direct[2], rtol=1e-6, atol=1e-7)
+
+
 # ------------------------------------------------------------- edge/contract
 def test_empty_inputs():
     shapes = torch.as_tensor([(4, 4), (2, 2)], dtype=torch.long, device=DEV)
