@@ -5,6 +5,13 @@
 
 #include <sys/mman.h>
 
+#include <algorithm>
+#include <random>
+
+// bounds of the LDS section (include/hip/hip_runtime.h: __shared__)
+extern "C" char __start_gd_emu_lds[] __attribute__((weak));
+extern "C" char __stop_gd_emu_lds[] __attribute__((weak));
+
 namespace gd_emu {
 namespace {
 
@@ -32,6 +39,32 @@ void release_if_complete() {
     g.arrived = 0;
     ++g.gen;
   }
+}
+
+enum class Sched { kFwd, kRev, kShuffle };
+Sched g_sched = Sched::kFwd;
+std::mt19937 g_rng;
+
+void read_sched_env() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* e = getenv("GD_EMU_SCHED");
+  if (!e || !*e || !strcmp(e, "fwd")) return;
+  if (!strcmp(e, "rev")) {
+    g_sched = Sched::kRev;
+  } else if (!strncmp(e, "shuffle:", 8)) {
+    g_sched = Sched::kShuffle;
+    g_rng.seed(unsigned(strtoul(e + 8, nullptr, 10)));
+  } else {
+    fprintf(stderr, "gd_emu: GD_EMU_SCHED=%s (want fwd | rev | shuffle:<seed>)\n", e);
+    abort();
+  }
+}
+
+void poison_lds() {
+  if (+__start_gd_emu_lds && +__stop_gd_emu_lds && +__stop_gd_emu_lds > +__start_gd_emu_lds)
+    memset(__start_gd_emu_lds, 0xFF, size_t(__stop_gd_emu_lds - __start_gd_emu_lds));
 }
 
 void trampoline() {
@@ -77,6 +110,9 @@ void run(dim3 gd, dim3 bd, void (*body)(void*), void* arg) {
   g.body = body;
   g.body_arg = arg;
   g.items.resize(n);
+  read_sched_env();
+  std::vector<unsigned> order(n);
+  for (unsigned i = 0; i < n; ++i) order[i] = g_sched == Sched::kRev ? n - 1 - i : i;
   for (unsigned bz = 0; bz < gd.z; ++bz)
     for (unsigned by = 0; by < gd.y; ++by)
       for (unsigned bx = 0; bx < gd.x; ++bx) {
@@ -95,9 +131,11 @@ void run(dim3 gd, dim3 bd, void (*body)(void*), void* arg) {
         }
         g.live = n;
         g.arrived = 0;
+        poison_lds();
         while (g.live > 0) {
           const uint64_t before = g_progress;
-          for (unsigned i = 0; i < n; ++i) {
+          if (g_sched == Sched::kShuffle) std::shuffle(order.begin(), order.end(), g_rng);
+          for (unsigned i : order) {
             if (g.items[i].done) continue;
             g.cur = i;
             swapcontext(&g.sched, &g.items[i].ctx);

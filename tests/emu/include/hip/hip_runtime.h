@@ -19,6 +19,10 @@
 // Wave = 64 consecutive work-items.  LDS (__shared__) is a static array,
 // zero-initialised once, like uninitialised LDS it must be written before use.
 // Global float atomics are plain read-modify-writes (one OS thread).
+// GD_EMU_SCHED=rev | shuffle:<seed> changes the order in which the scheduler
+// resumes work-items between synchronisation points (default: ascending):
+// a kernel missing a barrier between an LDS producer and a consumer in
+// another wave computes different results under another order.
 #pragma once
 
 #include <ucontext.h>
@@ -37,7 +41,11 @@
 #define __host__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
-#define __shared__ static
+// LDS arrays live in their own section so the scheduler can poison them
+// (0xFF bytes: NaN floats, -1 ints) before every workgroup: a kernel that
+// reads LDS it has not written in the same workgroup sees garbage, as on the
+// GPU, instead of the previous workgroup's values.
+#define __shared__ static __attribute__((section("gd_emu_lds")))
 
 struct dim3 {
   unsigned x, y, z;

@@ -154,6 +154,35 @@ def test_emulated_biattn_softmax(dtype, tol, shape):
     assert E.rel_err(ds.double(), sd.grad) < (1e-5 if dtype == torch.float32 else 3e-2)
 
 
+# ------------------------------------------------- scheduling perturbation
+_SCHED_SCRIPT = r"""
+import sys
+sys.path[:0] = {paths!r}
+import torch
+import test_emu_kernels as t
+S = sum(h * w for h, w in t.MEDIUM)
+t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=11, local=True, outlier_frac=0.1), 1e-5)
+t._check_bwd(t._levels_inputs(t.SMALL, 1, sum(h * w for h, w in t.SMALL), seed=12), 1e-5)
+t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 29, seed=13), 1e-5)
+t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 2, 300, 40))
+t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 1, 130, 256))
+print("sched-ok")
+"""
+
+
+@pytest.mark.parametrize("sched", ["rev", "shuffle:7"])
+def test_emulated_kernels_under_other_schedules(sched):
+    """Work-items resumed in descending / shuffled order between
+    synchronisation points, with LDS poisoned before every workgroup: a
+    missing barrier or a read of LDS the workgroup never wrote changes the
+    results (the default ascending order could hide either)."""
+    paths = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "open-groundingdino_amd")]
+    env = dict(os.environ, GD_EMU_SCHED=sched)
+    r = subprocess.run([sys.executable, "-c", _SCHED_SCRIPT.format(paths=paths)], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0 and "sched-ok" in r.stdout, r.stderr[-4000:]
+
+
 # ------------------------------------------------------ AddressSanitizer
 _ASAN_SCRIPT = r"""
 import sys
