@@ -29,11 +29,16 @@
  *                        max shift, +-5e4 clamps, column max, -inf masks, the
  *                        two softmaxes) and its autograd backward
  *                        models/GroundingDINO/fuse_modules.py:174-217
+ *   gd_window_attn_forward / _backward
+ *                     <- WindowAttention.forward core (q.scale.k^T, relative
+ *                        position bias gather, shift mask, softmax, attn.v)
+ *                        and its autograd backward incl. the scatter into
+ *                        relative_position_bias_table
+ *                        models/GroundingDINO/backbone/swin_transformer.py:134-174
  *
  * Not (yet) in this ABI version — these run as hipBLASLt GEMMs / PyTorch
- * SDPA compositions on the device: Swin window attention
- * (swin_transformer.py:134-174), BERT / text-enhancer / decoder attention,
- * ContrastiveEmbed (utils.py:242-273).
+ * SDPA compositions on the device: BERT / text-enhancer /
+ * decoder attention, ContrastiveEmbed (utils.py:242-273).
  */
 #ifndef GDINO_AMD_H
 #define GDINO_AMD_H
@@ -123,6 +128,33 @@ gd_status gd_biattn_softmax_fwd(gd_dtype dtype, const void* s, const uint8_t* pa
 gd_status gd_biattn_softmax_bwd(gd_dtype dtype, const void* pv, const void* pl, const void* dpv,
                                 const void* dpl, int B, int H, int S, int T, void* ds,
                                 void* workspace, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Swin window attention (swin_transformer.py:134-174)                       */
+/* ------------------------------------------------------------------------ */
+/*
+ * qkv       [B_, N, 3, nH, head_dim] the qkv Linear output (F32 or BF16,
+ *           16-byte aligned), windows of one image consecutive
+ * table     [(2Wh-1)(2Ww-1), nH] F32 relative_position_bias_table
+ * rel_index [N*N] int64 relative_position_index
+ * mask      [nW, N, N] F32 shift mask (0 / -100) or NULL; window b uses
+ *           mask[b % nW]; B_ % nW == 0
+ * out       [B_, N, nH*head_dim] (qkv dtype);  lse [B_, nH, N] F32 (softmax
+ *           log-sum-exp, input of the backward)
+ * N <= 64, head_dim == 32 (every Swin-T/S/B/L head); scale = head_dim^-0.5
+ * unless qk_scale is set.
+ */
+gd_status gd_window_attn_forward(gd_dtype dtype, const void* qkv, const float* table,
+                                 const int64_t* rel_index, const float* mask, int B_, int N,
+                                 int nH, int head_dim, int nW, float scale, void* out, float* lse,
+                                 gd_stream_t stream);
+/* grad_qkv [B_, N, 3, nH, head_dim] is written (every real token);
+ * grad_table [(2Wh-1)(2Ww-1), nH] F32 is ACCUMULATED into (zero it first). */
+gd_status gd_window_attn_backward(gd_dtype dtype, const void* qkv, const float* table,
+                                  const int64_t* rel_index, const float* mask, const void* out,
+                                  const void* grad_out, const float* lse, int B_, int N, int nH,
+                                  int head_dim, int nW, float scale, void* grad_qkv,
+                                  float* grad_table, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

@@ -4,6 +4,8 @@ Every model module calls the ops below instead of composing them from torch
 primitives, so that the implementation behind each op is one swap:
 
   window_attention   Swin W-MSA / SW-MSA core   swin_transformer.py:134-174
+  window_attention_packed  the same on the packed qkv Linear output with the
+                     bias table + index (what WindowAttention.forward calls)
   attention          masked SDPA (BERT self-attn, text enhancer, decoder
                      self-attn and text cross-attn)
   bi_attention       BiMultiHeadAttention core   fuse_modules.py:162-246
@@ -118,6 +120,12 @@ def window_attention(q, k, v, bias, mask, scale):
     return get("window_attention")(q, k, v, bias, mask, scale)
 
 
+def window_attention_packed(qkv, table, rel_index, mask, scale):
+    """qkv [B_, N, 3, nH, hd], table [(2Wh-1)(2Ww-1), nH], rel_index [N*N],
+    mask [nW, N, N] or None -> [B_, N, nH*hd] (gdino_amd/wattn.py)."""
+    return get("window_attention_packed")(qkv, table, rel_index, mask, scale)
+
+
 def attention(q, k, v, attn_mask=None, scale=None, dropout_p=0.0):
     return get("attention")(q, k, v, attn_mask, scale, dropout_p)
 
@@ -132,3 +140,4 @@ def contrastive_logits(x, text, text_token_mask, max_text_len):
 
 # HIP implementations register themselves as the defaults for CUDA tensors.
 from . import biattn  # noqa: E402,F401
+from . import wattn  # noqa: E402,F401

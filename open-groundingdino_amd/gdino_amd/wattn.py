@@ -1,0 +1,96 @@
+"""Swin W-MSA / SW-MSA core on MI355X: csrc/wattn.hip through the C-ABI.
+
+    out = softmax(q.scale.k^T + table[rel_index] (+ shift mask)) . v
+
+for every (window, head), as ONE MFMA kernel per direction, replacing the
+eager chain of the reference's WindowAttention.forward
+(backbone/swin_transformer.py:134-174): the [nH, N, N] bias gather +
+permute copy, q.k^T, two broadcast adds, softmax and attn.v, and in the
+backward their gradients plus the index_put scatter into
+relative_position_bias_table.
+
+Contract of ``window_attention_packed(qkv, table, rel_index, mask, scale)``:
+  qkv        [B_, N, 3, nH, hd]  the qkv Linear output, read in place
+  table      [(2Wh-1)(2Ww-1), nH] relative_position_bias_table (fp32 param)
+  rel_index  [N*N] int64          relative_position_index
+  mask       [nW, N, N] or None   0 / -100 shift mask, windows of one image
+                                  consecutive (window b uses mask[b % nW])
+  -> [B_, N, nH*hd]               the layout the proj Linear reads
+
+The HIP kernel covers N <= 64 (window <= 8) and hd = 32 (every Swin-T/S/B/L
+head) in fp32 and bf16.  Other shapes (Swin-B/384's 12x12 windows, N = 144)
+and dtypes use the torch composition (ROCm library kernels); CPU tensors
+raise, like every HIP op of this package.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib, kernels
+
+_p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+_lib.register("gd_window_attn_forward", [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _p, _p, _p])
+_lib.register("gd_window_attn_backward", [_i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _p, _p, _p])
+
+MAX_TOKENS = 64
+
+
+def supported(qkv: torch.Tensor) -> bool:
+    _, n, _, _, hd = qkv.shape
+    return qkv.dtype in (torch.float32, torch.bfloat16) and n <= MAX_TOKENS and hd == 32
+
+
+class WindowAttnFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, table, rel_index, mask, scale):
+        _lib.require_device(qkv, table, rel_index, mask, what="window_attention")
+        qkv = qkv.contiguous()
+        table32 = table.detach().float().contiguous()
+        ridx = rel_index.to(torch.int64).contiguous()
+        mask32 = None if mask is None else mask.float().contiguous()
+        b_, n, _, nh, hd = qkv.shape
+        nw = 1 if mask32 is None else mask32.shape[0]
+        out = torch.empty(b_, n, nh * hd, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(b_, nh, n, dtype=torch.float32, device=qkv.device)
+        _lib.call("gd_window_attn_forward", _lib.dtype_code(qkv), qkv.data_ptr(), table32.data_ptr(),
+                  ridx.data_ptr(), _lib.ptr(mask32), b_, n, nh, hd, nw, float(scale), out.data_ptr(),
+                  lse.data_ptr(), _lib.stream_of(qkv))
+        ctx.save_for_backward(qkv, table32, ridx, mask32, out, lse)
+        ctx.scale = float(scale)
+        ctx.table_dtype = table.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, table32, ridx, mask32, out, lse = ctx.saved_tensors
+        b_, n, _, nh, hd = qkv.shape
+        nw = 1 if mask32 is None else mask32.shape[0]
+        dout = dout.to(qkv.dtype).contiguous()
+        dqkv = torch.empty_like(qkv)
+        dtable = torch.zeros_like(table32)
+        _lib.call("gd_window_attn_backward", _lib.dtype_code(qkv), qkv.data_ptr(), table32.data_ptr(),
+                  ridx.data_ptr(), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), b_, n, nh,
+                  hd, nw, ctx.scale, dqkv.data_ptr(), dtable.data_ptr(), _lib.stream_of(qkv))
+        return dqkv, dtable.to(ctx.table_dtype), None, None, None
+
+
+def window_attention_packed_hip(qkv, table, rel_index, mask, scale):
+    if not supported(qkv):
+        return window_attention_packed_torch(qkv, table, rel_index, mask, scale)
+    return WindowAttnFunction.apply(qkv, table, rel_index, mask, scale)
+
+
+def window_attention_packed_torch(qkv, table, rel_index, mask, scale):
+    """The same op composed from ROCm library kernels (shapes the HIP kernel
+    does not cover)."""
+    b_, n, _, nh, hd = qkv.shape
+    q, k, v = qkv.permute(2, 0, 3, 1, 4)
+    bias = table[rel_index.view(-1)].view(n, n, nh).permute(2, 0, 1).contiguous()
+    out = kernels._window_attention_torch(q, k, v, bias, mask, scale)
+    return out.transpose(1, 2).reshape(b_, n, nh * hd)
+
+
+kernels.register("window_attention_packed", "torch", window_attention_packed_torch)
+kernels.register("window_attention_packed", "hip", window_attention_packed_hip, default=True)

@@ -89,9 +89,23 @@ class WindowAttention(nn.Module):
     def forward(self, x, mask=None):
         """x: [B*nW, N, C]; mask: [nW, N, N] (0 / -100) or None."""
         b_, n, c = x.shape
-        qkv = self.qkv(x).view(b_, n, 3, self.num_heads, c // self.num_heads).permute(2, 0, 3, 1, 4)
-        out = kernels.window_attention(qkv[0], qkv[1], qkv[2], self.position_bias(), mask, self.scale)
-        out = out.transpose(1, 2).reshape(b_, n, c)
+        qkv = self.qkv(x).view(b_, n, 3, self.num_heads, c // self.num_heads)
+        if self.attn_drop.p > 0.0 and self.training:
+            # attention-probability dropout (attn_drop_rate > 0; 0 in every
+            # Grounding DINO config) is not fused: eager composition
+            q, k, v = qkv.permute(2, 0, 3, 1, 4)
+            attn = (q * self.scale) @ k.transpose(-2, -1) + self.position_bias().unsqueeze(0).to(q.dtype)
+            if mask is not None:
+                nw = mask.shape[0]
+                attn = (attn.view(b_ // nw, nw, self.num_heads, n, n) + mask.to(attn.dtype)[None, :, None])
+                attn = attn.view(b_, self.num_heads, n, n)
+            out = (self.attn_drop(attn.softmax(-1)) @ v).transpose(1, 2).reshape(b_, n, c)
+        else:
+            # one fused kernel: bias gather, shift mask, softmax, both products
+            # (gdino_amd/wattn.py, csrc/wattn.hip); reads qkv in place, writes
+            # the [B_, N, C] layout proj reads
+            out = kernels.window_attention_packed(qkv, self.relative_position_bias_table,
+                                                  self.relative_position_index.view(-1), mask, self.scale)
         return self.proj_drop(self.proj(out))
 
 

@@ -9,6 +9,7 @@ reference module imports here (tests/golden/make_block_golden.py).
   bi_attention_ref     fuse_modules.py:162-246 (global max shift, +-5e4
                        clamps, column-max shift, -inf masks, two softmaxes)
   window_attention_ref swin_transformer.py:134-174
+  window_attention_packed_ref  the same on the packed qkv + bias table (:113-114, :171)
   attention_ref        masked softmax(q k^T * scale) v (additive / bool mask)
   contrastive_ref      utils.py:242-273
   phrase_masks_ref     bertwarper.py:224-273 (per-special-token loop)
@@ -56,6 +57,17 @@ def window_attention_ref(q, k, v, bias, mask, scale):
         attn = attn.view(b_ // nw, nw, nh, n, n) + mask.unsqueeze(1).unsqueeze(0)
         attn = attn.view(-1, nh, n, n)
     return torch.softmax(attn, dim=-1) @ v
+
+
+def window_attention_packed_ref(qkv, table, rel_index, mask, scale):
+    """WindowAttention.forward core (swin_transformer.py:134-174) on the packed
+    qkv [B_, N, 3, nH, hd] with the bias table [(2Wh-1)(2Ww-1), nH] and
+    rel_index [N*N] (:113-114) -> [B_, N, nH*hd] (:171)."""
+    b_, n, _, nh, hd = qkv.shape
+    q, k, v = qkv.permute(2, 0, 3, 1, 4)
+    bias = table[rel_index.view(-1)].view(n, n, -1).permute(2, 0, 1).contiguous()
+    out = window_attention_ref(q, k, v, bias, mask, scale)
+    return out.transpose(1, 2).reshape(b_, n, nh * hd)
 
 
 def attention_ref(q, k, v, mask=None, scale=None):

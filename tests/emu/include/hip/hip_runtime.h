@@ -12,8 +12,9 @@
 // Model: one workgroup at a time; each work-item is a ucontext fiber on one OS
 // thread, scheduled round-robin.  A fiber runs until it has to wait:
 //   * __syncthreads(): until every live work-item of the block has arrived;
-//   * cross-lane reads (__shfl_xor, ds_swizzle, DPP): until the source lane
-//     has published its value for the same exchange (each lane publishes into
+//   * cross-lane reads (__shfl_xor, ds_swizzle, DPP) and MFMA (whose
+//     operands come from all 64 lanes): until the source lane(s) have
+//     published their value for the same exchange (each lane publishes into
 //     an append-only log indexed by its exchange count, so a source never
 //     overwrites a value a slower reader still needs).
 // Wave = 64 consecutive work-items.  LDS (__shared__) is a static array,
@@ -58,6 +59,8 @@ struct uint4 { unsigned x, y, z, w; };
 inline float2 make_float2(float a, float b) { return {a, b}; }
 inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
 inline uint2 make_uint2(unsigned a, unsigned b) { return {a, b}; }
+inline uint4 make_uint4(unsigned a, unsigned b, unsigned c, unsigned d) { return {a, b, c, d}; }
+inline float __logf(float x) { return logf(x); }
 
 typedef int hipError_t;
 constexpr hipError_t hipSuccess = 0;
@@ -206,6 +209,86 @@ inline V shfl_xor(V v, int mask, int width) {
   return xchg_from(v, wave_base() + src);
 }
 
+// All 64 lanes of the caller's wave contribute `nbytes` (<= 64) and every
+// lane receives the 64 contributions in lane order (MFMA operand exchange).
+inline void wave_gather(const void* mine, size_t nbytes, void* all) {
+  Grid& g = grid();
+  const size_t nw = (nbytes + 7) / 8;
+  uint64_t w[8] = {};
+  memcpy(w, mine, nbytes);
+  const size_t k0 = g.items[g.cur].nxchg;
+  for (size_t i = 0; i < nw; ++i) g.items[g.cur].published.push_back(w[i]);
+  g.items[g.cur].nxchg += nw;
+  note_progress();
+  const unsigned base = wave_base();
+  if (base + 64 > g.items.size()) {
+    fprintf(stderr, "gd_emu: MFMA in a partial wave (block of %zu work-items)\n", g.items.size());
+    abort();
+  }
+  for (unsigned s = 0; s < 64; ++s) {
+    for (;;) {
+      Item& o = g.items[base + s];
+      if (o.published.size() >= k0 + nw) {
+        memcpy(static_cast<char*>(all) + s * nbytes, &o.published[k0], nbytes);
+        break;
+      }
+      if (o.done) {
+        fprintf(stderr, "gd_emu: MFMA of work-item %u waits for exited work-item %u\n", flat_id(), base + s);
+        abort();
+      }
+      yield();
+    }
+  }
+}
+
+inline float bf16_bits_to_f(uint16_t h) {
+  uint32_t u = uint32_t(h) << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// v_mfma_f32_16x16x32_bf16 (cdna_hip_programming.md §3, lane maps [HW]):
+// lane l holds A[l&15][8(l>>4)+j] and B[8(l>>4)+j][l&15] in element j, and
+// receives D[4(l>>4)+r][l&15] in element r.  Products are exact; the sum is
+// taken in double and rounded once.
+template <typename V8, typename C4>
+inline C4 mfma_16x16x32_bf16(V8 a, V8 b, C4 c) {
+  static_assert(sizeof(V8) == 16 && sizeof(C4) == 16, "bf16x8 / f32x4 operands");
+  struct Ops { uint16_t a[8], b[8]; } mine, all[64];
+  memcpy(mine.a, &a, 16);
+  memcpy(mine.b, &b, 16);
+  wave_gather(&mine, sizeof(Ops), all);
+  const unsigned l = lane_id();
+  C4 d;
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * int(l >> 4) + r, col = int(l & 15);
+    double acc = 0.0;
+    for (int k = 0; k < 32; ++k)
+      acc += double(bf16_bits_to_f(all[row + 16 * (k >> 3)].a[k & 7])) *
+             double(bf16_bits_to_f(all[col + 16 * (k >> 3)].b[k & 7]));
+    d[r] = float(double(c[r]) + acc);
+  }
+  return d;
+}
+
+// v_mfma_f32_16x16x4_f32: lane l holds A[l&15][l>>4] and B[l>>4][l&15].
+template <typename C4>
+inline C4 mfma_16x16x4_f32(float a, float b, C4 c) {
+  static_assert(sizeof(C4) == 16, "f32x4 accumulator");
+  struct Ops { float a, b; } mine{a, b}, all[64];
+  wave_gather(&mine, sizeof(Ops), all);
+  const unsigned l = lane_id();
+  C4 d;
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * int(l >> 4) + r, col = int(l & 15);
+    double acc = 0.0;
+    for (int k = 0; k < 4; ++k) acc += double(all[row + 16 * k].a) * double(all[col + 16 * k].b);
+    d[r] = float(double(c[r]) + acc);
+  }
+  return d;
+}
+
 void syncthreads();
 
 template <typename F>
@@ -225,6 +308,9 @@ void launch(dim3 g, dim3 b, F&& f) {
 #define __builtin_amdgcn_ds_swizzle(v, pattern) ::gd_emu::ds_swizzle((v), (pattern))
 #define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) \
   ::gd_emu::update_dpp((old), (src), (ctrl), (rm), (bm), (bc))
+#define __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, cbsz, abid, blgp) \
+  ::gd_emu::mfma_16x16x32_bf16((a), (b), (c))
+#define __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, cbsz, abid, blgp) ::gd_emu::mfma_16x16x4_f32((a), (b), (c))
 #define hipLaunchKernelGGL(kernel, g, b, shm, stream, ...) \
   ((void)(shm), (void)(stream), ::gd_emu::launch(dim3(g), dim3(b), [&]() { kernel(__VA_ARGS__); }))
 

@@ -33,6 +33,9 @@ def lib():
         _LIB.gd_biattn_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_biattn_softmax_fwd.argtypes = [_i, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]
         _LIB.gd_biattn_softmax_bwd.argtypes = [_i, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p]
+        _LIB.gd_window_attn_forward.argtypes = [_i, _p, _p, _p, _p] + [_i] * 5 + [ctypes.c_float, _p, _p, _p]
+        _LIB.gd_window_attn_backward.argtypes = ([_i, _p, _p, _p, _p, _p, _p, _p] + [_i] * 5 +
+                                                 [ctypes.c_float, _p, _p, _p])
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -101,6 +104,35 @@ def biattn_softmax_bwd(pv, pl, dpv, dpl):
     _check(lib().gd_biattn_softmax_bwd(_code(pv), _ptr(pv), _ptr(pl), _ptr(dpv), _ptr(dpl), B, H, S, T, _ptr(ds),
                                        _ptr(ws), None))
     return ds
+
+
+def window_attn_forward(qkv, table, ridx, mask, scale):
+    """qkv [B_, N, 3, nH, hd] (f32/bf16), table [R, nH] f32, ridx [N*N] int64,
+    mask [nW, N, N] f32 or None -> out [B_, N, nH*hd], lse [B_, nH, N]."""
+    B_, N, _, nH, hd = qkv.shape
+    nW = 1 if mask is None else mask.shape[0]
+    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    mask = None if mask is None else mask.float().contiguous()
+    out = torch.empty(B_, N, nH * hd, dtype=qkv.dtype)
+    lse = torch.empty(B_, nH, N, dtype=torch.float32)
+    _check(lib().gd_window_attn_forward(_code(qkv), _ptr(qkv), _ptr(table), _ptr(ridx), _ptr(mask), B_, N, nH, hd,
+                                        nW, scale, _ptr(out), _ptr(lse), None))
+    return out, lse
+
+
+def window_attn_backward(qkv, table, ridx, mask, scale, out, lse, grad_out):
+    """-> grad_qkv (qkv dtype), grad_table (f32, [R, nH])."""
+    B_, N, _, nH, hd = qkv.shape
+    nW = 1 if mask is None else mask.shape[0]
+    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    mask = None if mask is None else mask.float().contiguous()
+    out, lse, grad_out = out.contiguous(), lse.contiguous(), grad_out.contiguous()
+    gq = torch.full_like(qkv, float("nan"))
+    gt = torch.zeros_like(table)
+    _check(lib().gd_window_attn_backward(_code(qkv), _ptr(qkv), _ptr(table), _ptr(ridx), _ptr(mask), _ptr(out),
+                                         _ptr(grad_out), _ptr(lse), B_, N, nH, hd, nW, scale, _ptr(gq), _ptr(gt),
+                                         None))
+    return gq, gt
 
 
 def rel_err(a, b):

@@ -1,5 +1,5 @@
-"""Test-only: run the model's host logic on CPU by routing the HIP-only MSDA
-op to the oracle restatement.  The product raises on CPU tensors; this hook
+"""Test-only: run the model's host logic on CPU by routing the HIP-only ops
+(MSDA, BiAttention softmax, window attention) to their oracle restatements.  The product raises on CPU tensors; this hook
 is the only way CPU tests execute MSDA."""
 import contextlib
 
@@ -17,13 +17,14 @@ def oracle_msda():
     """Route every HIP-only op to its oracle restatement (CPU tests)."""
     import models.GroundingDINO.ms_deform_attn as mod
     from gdino_amd import kernels
-    from oracle.blocks import bi_attention_ref
+    from oracle.blocks import bi_attention_ref, window_attention_packed_ref
 
     prev = mod.MSDeformAttnFunction
     mod.MSDeformAttnFunction = _OracleMSDA
     try:
         with kernels.override("bi_attention", lambda q, k, vv, vl, pv=None, pl=None, p=0.0:
-                              bi_attention_ref(q, k, vv, vl, pv, pl)):
+                              bi_attention_ref(q, k, vv, vl, pv, pl)), \
+                kernels.override("window_attention_packed", window_attention_packed_ref):
             yield
     finally:
         mod.MSDeformAttnFunction = prev

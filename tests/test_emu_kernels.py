@@ -166,6 +166,8 @@ t._check_bwd(t._levels_inputs(t.SMALL, 1, sum(h * w for h, w in t.SMALL), seed=1
 t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 29, seed=13), 1e-5)
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 2, 300, 40))
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 1, 130, 256))
+t.test_emulated_window_attention(7, 3, 8, 4, True, torch.float32, 1e-5)
+t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
 print("sched-ok")
 """
 
@@ -195,6 +197,8 @@ t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, 
 t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 37, seed=6), 1e-5)
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 2, 200, 100))
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
+t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)
+t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
 print("asan-clean")
 """
 
@@ -214,3 +218,58 @@ def test_emulated_kernels_under_address_sanitizer():
     r = subprocess.run([sys.executable, "-c", _ASAN_SCRIPT.format(paths=paths)], env=env, capture_output=True,
                        text=True, timeout=900)
     assert r.returncode == 0 and "asan-clean" in r.stdout, r.stderr[-4000:]
+
+
+# ------------------------------------------- Swin window attention (MFMA)
+def _wattn_case(ws, nH, B_, nW, masked, seed, dtype):
+    from models.GroundingDINO.backbone.swin_transformer import relative_position_index
+    g = torch.Generator().manual_seed(seed)
+    N, hd = ws * ws, 32
+    qkv = torch.randn(B_, N, 3, nH, hd, generator=g).to(dtype)
+    table = torch.randn((2 * ws - 1) ** 2, nH, generator=g) * 0.5
+    ridx = relative_position_index(ws, ws).reshape(-1)
+    mask = torch.where(torch.rand(nW, N, N, generator=g) < 0.3, -100.0, 0.0) if masked else None
+    grad = torch.randn(B_, N, nH * hd, generator=g).to(dtype)
+    return qkv, table, ridx, mask, hd ** -0.5, grad
+
+
+def _wattn_ref(qkv, table, ridx, mask, scale):
+    """reference WindowAttention.forward core (swin_transformer.py:134-174), fp64"""
+    B_, N, _, nH, hd = qkv.shape
+    q, k, v = qkv.permute(2, 0, 3, 1, 4)
+    attn = (q * scale) @ k.transpose(-1, -2) + table[ridx].view(N, N, nH).permute(2, 0, 1)
+    if mask is not None:
+        nW = mask.shape[0]
+        attn = (attn.view(B_ // nW, nW, nH, N, N) + mask[None, :, None]).view(B_, nH, N, N)
+    return (attn.softmax(-1) @ v).transpose(1, 2).reshape(B_, N, nH * hd)
+
+
+@pytest.mark.parametrize("ws,nH,B_,nW,masked,dtype,tol", [
+    (7, 3, 8, 4, True, torch.float32, 1e-5),     # Swin-T stage 0 heads, shifted windows
+    (7, 2, 22, 1, False, torch.float32, 1e-5),   # tail blocks (B_ not a multiple of 16)
+    (8, 1, 4, 2, True, torch.float32, 1e-5),     # N = 64: no padded tokens
+    (3, 4, 6, 3, True, torch.float32, 1e-5),     # N = 9: mostly padding
+    (7, 3, 8, 4, True, torch.bfloat16, 1.5e-2),  # the training dtype
+    (5, 2, 20, 5, False, torch.bfloat16, 1.5e-2),
+])
+def test_emulated_window_attention(ws, nH, B_, nW, masked, dtype, tol):
+    qkv, table, ridx, mask, scale, grad = _wattn_case(ws, nH, B_, nW, masked, seed=ws * 100 + B_, dtype=dtype)
+    out, lse = E.window_attn_forward(qkv, table, ridx, mask, scale)
+    qd = qkv.double().requires_grad_(True)
+    td = table.double().requires_grad_(True)
+    ref = _wattn_ref(qd, td, ridx, None if mask is None else mask.double(), scale)
+    assert E.rel_err(out.double(), ref.detach()) < tol
+    ref.backward(grad.double())
+    gq, gt = E.window_attn_backward(qkv, table, ridx, mask, scale, out, lse, grad)
+    assert torch.isfinite(gq).all()
+    assert E.rel_err(gq.double(), qd.grad) < tol * 2
+    assert E.rel_err(gt.double(), td.grad) < tol * 2
+
+
+def test_emulated_window_attention_rejects_bad_shapes():
+    qkv, table, ridx, mask, scale, _ = _wattn_case(7, 2, 8, 4, True, 0, torch.float32)
+    with pytest.raises(RuntimeError, match="multiple of nW"):
+        E.window_attn_forward(qkv[:6], table, ridx, mask, scale)
+    big = torch.zeros(2, 81, 3, 1, 32)
+    with pytest.raises(RuntimeError, match="bad sizes"):
+        E.window_attn_forward(big, torch.zeros(289, 1), torch.zeros(81 * 81, dtype=torch.long), None, 1.0)

@@ -202,3 +202,21 @@ def test_cast_cache_is_bit_identical_under_autocast(built):
     noise = max(rel(g0[n], gf[n]) for n in gf)
     fused = max(rel(g2[n], gf[n]) for n in gf)
     assert fused <= 1.25 * noise + 0.02, (fused, noise)
+
+
+def test_window_attention_packed_torch_composition_matches_oracle():
+    """The torch composition behind window_attention_packed (used for shapes
+    the HIP kernel does not cover) equals the reference restatement (fp64)."""
+    from gdino_amd.wattn import window_attention_packed_torch
+    from models.GroundingDINO.backbone.swin_transformer import relative_position_index
+    from oracle.blocks import window_attention_packed_ref
+    g = torch.Generator().manual_seed(0)
+    for ws, masked in ((7, True), (12, False)):
+        n = ws * ws
+        qkv = torch.randn(8, n, 3, 4, 32, generator=g, dtype=torch.float64)
+        table = torch.randn((2 * ws - 1) ** 2, 4, generator=g, dtype=torch.float64)
+        ridx = relative_position_index(ws, ws).reshape(-1)
+        mask = torch.where(torch.rand(4, n, n, generator=g) < 0.3, -100.0, 0.0).double() if masked else None
+        torch.testing.assert_close(window_attention_packed_torch(qkv, table, ridx, mask, 32 ** -0.5),
+                                   window_attention_packed_ref(qkv, table, ridx, mask, 32 ** -0.5),
+                                   rtol=1e-12, atol=1e-12)
