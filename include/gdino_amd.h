@@ -36,9 +36,16 @@
  *                        relative_position_bias_table
  *                        models/GroundingDINO/backbone/swin_transformer.py:134-174
  *
- * Not (yet) in this ABI version — these run as hipBLASLt GEMMs / PyTorch
- * SDPA compositions on the device: BERT / text-enhancer /
- * decoder attention, ContrastiveEmbed (utils.py:242-273).
+ *   gd_attn_forward / _backward
+ *                     <- the attention cores the reference runs as eager
+ *                        matmul / softmax / matmul: BERT self-attention (HF
+ *                        BertSelfAttention via bertwarper.py:31-166), the
+ *                        text enhancer's and the decoder's
+ *                        nn.MultiheadAttention (transformer_vanilla.py:83,
+ *                        transformer.py:839,844)
+ *
+ * Not (yet) in this ABI version — a hipBLASLt GEMM + masked_fill on the
+ * device: ContrastiveEmbed (utils.py:242-273).
  */
 #ifndef GDINO_AMD_H
 #define GDINO_AMD_H
@@ -155,6 +162,37 @@ gd_status gd_window_attn_backward(gd_dtype dtype, const void* qkv, const float* 
                                   const void* grad_out, const float* lse, int B_, int N, int nH,
                                   int head_dim, int nW, float scale, void* grad_qkv,
                                   float* grad_table, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Masked multi-head attention (flash-style; scores never reach HBM)         */
+/* ------------------------------------------------------------------------ */
+/*
+ * q [B, H, Lq, head_dim], k / v [B, H, Lk, head_dim] and out (and the
+ * gradients) are addressed through host arrays of 3 element strides
+ * (b, h, l); channels are contiguous and every row is 16-byte aligned.
+ * mask (mask_kind 1: uint8 keep-mask, 1 = attend; 2: additive F32; 0: none)
+ * is indexed [b, h, q, k] through 3 host strides (b, h, q), 0 for a
+ * broadcast dimension, and is contiguous along k.
+ * dtype F32 or BF16, head_dim 32 or 64, Lq, Lk > 0, B*H < 65536.
+ * lse [B, H, Lq] F32: per-row log-sum-exp (+inf for a row with every key
+ * masked, whose output is 0), input of the backward.
+ */
+gd_status gd_attn_forward(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                          const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                          const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                          const int64_t* mask_strides, float scale, void* out,
+                          const int64_t* out_strides, float* lse, gd_stream_t stream);
+/* dsum: [B, H, Lq] F32 workspace (rowsum(dO . O)); grad_q / grad_k / grad_v
+ * are fully written. */
+gd_status gd_attn_backward(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                           const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                           const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                           const int64_t* mask_strides, float scale, const void* out,
+                           const int64_t* out_strides, const void* grad_out,
+                           const int64_t* grad_out_strides, const float* lse, float* dsum,
+                           void* grad_q, const int64_t* grad_q_strides, void* grad_k,
+                           const int64_t* grad_k_strides, void* grad_v,
+                           const int64_t* grad_v_strides, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

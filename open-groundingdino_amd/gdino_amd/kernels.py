@@ -6,8 +6,8 @@ primitives, so that the implementation behind each op is one swap:
   window_attention   Swin W-MSA / SW-MSA core   swin_transformer.py:134-174
   window_attention_packed  the same on the packed qkv Linear output with the
                      bias table + index (what WindowAttention.forward calls)
-  attention          masked SDPA (BERT self-attn, text enhancer, decoder
-                     self-attn and text cross-attn)
+  attention          masked attention (BERT self-attn, text enhancer, decoder
+                     self-attn and text cross-attn): gdino_amd/attn.py
   bi_attention       BiMultiHeadAttention core   fuse_modules.py:162-246
   contrastive_logits ContrastiveEmbed            utils.py:242-273
 
@@ -141,3 +141,4 @@ def contrastive_logits(x, text, text_token_mask, max_text_len):
 # HIP implementations register themselves as the defaults for CUDA tensors.
 from . import biattn  # noqa: E402,F401
 from . import wattn  # noqa: E402,F401
+from . import attn  # noqa: E402,F401

@@ -36,6 +36,8 @@ def lib():
         _LIB.gd_window_attn_forward.argtypes = [_i, _p, _p, _p, _p] + [_i] * 5 + [ctypes.c_float, _p, _p, _p]
         _LIB.gd_window_attn_backward.argtypes = ([_i, _p, _p, _p, _p, _p, _p, _p] + [_i] * 5 +
                                                  [ctypes.c_float, _p, _p, _p])
+        _LIB.gd_attn_forward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, ctypes.c_float, _p, _p, _p, _p]
+        _LIB.gd_attn_backward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, ctypes.c_float] + [_p] * 13
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -133,6 +135,57 @@ def window_attn_backward(qkv, table, ridx, mask, scale, out, lse, grad_out):
                                          _ptr(grad_out), _ptr(lse), B_, N, nH, hd, nW, scale, _ptr(gq), _ptr(gt),
                                          None))
     return gq, gt
+
+
+def _st3(t):
+    return (ctypes.c_int64 * 3)(*t.stride()[:3])
+
+
+def _mask_args(mask):
+    """mask broadcastable to [B, H, Lq, Lk] (bool keep or additive float) ->
+    (tensor, kind, strides)"""
+    if mask is None:
+        return None, 0, None
+    m = mask if mask.dtype == torch.bool else mask.float()
+    while m.dim() < 4:
+        m = m.unsqueeze(0)
+    if m.stride(-1) != 1:
+        m = m.contiguous()
+    if m.dtype == torch.bool:
+        m = m.view(torch.uint8)
+        kind = 1
+    else:
+        kind = 2
+    st = [0 if m.shape[i] == 1 else m.stride(i) for i in range(3)]
+    return m, kind, (ctypes.c_int64 * 3)(*st)
+
+
+def attn_forward(q, k, v, mask, scale):
+    """q [B,H,Lq,hd], k/v [B,H,Lk,hd] (any (b,h,l) strides, contiguous hd)
+    -> out [B,H,Lq,hd] (stored [B,Lq,H,hd]), lse [B,H,Lq]"""
+    B, H, Lq, hd = q.shape
+    Lk = k.shape[2]
+    m, kind, ms = _mask_args(mask)
+    out = torch.empty(B, Lq, H, hd, dtype=q.dtype).transpose(1, 2)
+    lse = torch.empty(B, H, Lq, dtype=torch.float32)
+    _check(lib().gd_attn_forward(_code(q), B, H, Lq, Lk, hd, _ptr(q), _st3(q), _ptr(k), _st3(k), _ptr(v), _st3(v),
+                                 _ptr(m), kind, ms, scale, _ptr(out), _st3(out), _ptr(lse), None))
+    return out, lse
+
+
+def attn_backward(q, k, v, mask, scale, out, lse, grad_out):
+    B, H, Lq, hd = q.shape
+    Lk = k.shape[2]
+    m, kind, ms = _mask_args(mask)
+    dsum = torch.empty(B, H, Lq, dtype=torch.float32)
+    dq = torch.full_like(q, float("nan"))
+    dk = torch.full_like(k, float("nan"))
+    dv = torch.full_like(v, float("nan"))
+    _check(lib().gd_attn_backward(_code(q), B, H, Lq, Lk, hd, _ptr(q), _st3(q), _ptr(k), _st3(k), _ptr(v), _st3(v),
+                                  _ptr(m), kind, ms, scale, _ptr(out), _st3(out), _ptr(grad_out), _st3(grad_out),
+                                  _ptr(lse), _ptr(dsum), _ptr(dq), _st3(dq), _ptr(dk), _st3(dk), _ptr(dv), _st3(dv),
+                                  None))
+    return dq, dk, dv
 
 
 def rel_err(a, b):

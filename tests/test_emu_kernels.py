@@ -168,6 +168,7 @@ t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 2, 300, 40))
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 1, 130, 256))
 t.test_emulated_window_attention(7, 3, 8, 4, True, torch.float32, 1e-5)
 t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
+t.test_emulated_attention(2, 2, 100, 130, 64, "bool", torch.float32, 1e-5, "lbh")
 print("sched-ok")
 """
 
@@ -199,6 +200,8 @@ t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 2, 200, 100))
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
 t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)
 t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
+t.test_emulated_attention(2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh")
+t.test_emulated_attention(1, 1, 33, 300, 32, "add", torch.float32, 1e-5, "blh")
 print("asan-clean")
 """
 
@@ -273,3 +276,70 @@ def test_emulated_window_attention_rejects_bad_shapes():
     big = torch.zeros(2, 81, 3, 1, 32)
     with pytest.raises(RuntimeError, match="bad sizes"):
         E.window_attn_forward(big, torch.zeros(289, 1), torch.zeros(81 * 81, dtype=torch.long), None, 1.0)
+
+
+# ------------------------------- masked multi-head attention (flash, MFMA)
+def _attn_case(B, H, Lq, Lk, hd, mask_kind, dtype, seed, layout="lbh"):
+    g = torch.Generator().manual_seed(seed)
+
+    def proj(L):  # the MHA / BERT projection layouts, read in place
+        if layout == "lbh":
+            return torch.randn(L, B, H, hd, generator=g).to(dtype).permute(1, 2, 0, 3)
+        return torch.randn(B, L, H, hd, generator=g).to(dtype).transpose(1, 2)
+
+    q, k, v = proj(Lq), proj(Lk), proj(Lk)
+    if mask_kind == "none":
+        mask = None
+    elif mask_kind == "keypad":  # [B, 1, 1, Lk] bool, the decoder's text cross-attention
+        mask = torch.ones(B, 1, 1, Lk, dtype=torch.bool)
+        mask[-1, ..., Lk // 2:] = False
+    elif mask_kind == "bool":  # [B, H, Lq, Lk] (text enhancer / BERT phrase blocks)
+        mask = torch.rand(B, H, Lq, Lk, generator=g) < 0.7
+        mask[..., 0] = True
+    elif mask_kind == "dead_rows":  # some rows attend nothing
+        mask = torch.rand(B, 1, Lq, Lk, generator=g) < 0.7
+        mask[:, :, 3] = False
+    else:  # additive float [B, 1, Lq, Lk] (BERT extended mask)
+        mask = torch.where(torch.rand(B, 1, Lq, Lk, generator=g) < 0.2, -1e4, 0.0)
+    grad = torch.randn(B, H, Lq, hd, generator=g).to(dtype)
+    return q, k, v, mask, hd ** -0.5, grad
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,mask_kind,dtype,tol,layout", [
+    (1, 2, 70, 50, 32, "none", torch.float32, 1e-5, "lbh"),
+    (2, 2, 100, 130, 64, "bool", torch.float32, 1e-5, "lbh"),
+    (1, 1, 33, 300, 32, "add", torch.float32, 1e-5, "blh"),
+    (2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh"),   # decoder text cross-attention shape class
+    (1, 2, 64, 64, 64, "bool", torch.bfloat16, 1.5e-2, "blh"),   # BERT shape class
+    (2, 1, 90, 70, 32, "keypad", torch.bfloat16, 1.5e-2, "lbh"),
+])
+def test_emulated_attention(B, H, Lq, Lk, hd, mask_kind, dtype, tol, layout):
+    from oracle.blocks import attention_ref
+    q, k, v, mask, scale, grad = _attn_case(B, H, Lq, Lk, hd, mask_kind, dtype, seed=Lq + Lk, layout=layout)
+    out, lse = E.attn_forward(q, k, v, mask, scale)
+    qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
+    md = None if mask is None else (mask if mask.dtype == torch.bool else mask.double())
+    ref = attention_ref(qd, kd, vd, md, scale)
+    assert E.rel_err(out.double(), ref.detach()) < tol
+    ref.backward(grad.double())
+    dq, dk, dv = E.attn_backward(q, k, v, mask, scale, out, lse, grad)
+    for name, mine, r in (("dq", dq, qd.grad), ("dk", dk, kd.grad), ("dv", dv, vd.grad)):
+        assert torch.isfinite(mine).all(), name
+        assert E.rel_err(mine.double(), r) < tol * 2, name
+
+
+def test_emulated_attention_fully_masked_rows_are_zero():
+    """A query row whose keys are all masked gives 0 output and 0 gradients
+    (the reference's softmax would give NaN there; no caller produces such
+    rows: every caption keeps its [CLS] token)."""
+    from oracle.blocks import attention_ref
+    q, k, v, mask, scale, grad = _attn_case(1, 2, 20, 30, 32, "dead_rows", torch.float32, seed=3)
+    out, lse = E.attn_forward(q, k, v, mask, scale)
+    assert torch.equal(out[:, :, 3], torch.zeros_like(out[:, :, 3]))
+    live = torch.ones(20, dtype=torch.bool)
+    live[3] = False
+    ref = attention_ref(q.double(), k.double(), v.double(), mask, scale)
+    assert E.rel_err(out[:, :, live].double(), ref[:, :, live]) < 1e-5
+    dq, dk, dv = E.attn_backward(q, k, v, mask, scale, out, lse, grad)
+    assert torch.isfinite(dq).all() and torch.isfinite(dk).all() and torch.isfinite(dv).all()
+    assert torch.equal(dq[:, :, 3], torch.zeros_like(dq[:, :, 3]))

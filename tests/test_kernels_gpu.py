@@ -124,3 +124,64 @@ def test_window_attention_rejects_host_tensors():
     qkv, table, ridx, mask = _wattn_inputs(7, 2, 4, 2, True, torch.float32)
     with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
         WindowAttnFunction.apply(qkv, table, ridx, mask, 1.0)
+
+
+# ------------------------------------- masked multi-head attention (HIP)
+def _attn_inputs(b, h, lq, lk, hd, mask_kind, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(lq, b, h, hd, generator=g).to(dtype).permute(1, 2, 0, 3)  # MHA projection layout
+    k = torch.randn(lk, b, h, hd, generator=g).to(dtype).permute(1, 2, 0, 3)
+    v = torch.randn(lk, b, h, hd, generator=g).to(dtype).permute(1, 2, 0, 3)
+    if mask_kind == "keypad":
+        mask = torch.ones(b, 1, 1, lk, dtype=torch.bool)
+        mask[-1, ..., lk // 2:] = False
+    elif mask_kind == "bool":
+        mask = torch.rand(b, h, lq, lk, generator=g) < 0.7
+        mask[..., 0] = True
+    elif mask_kind == "add":
+        mask = torch.where(torch.rand(b, 1, lq, lk, generator=g) < 0.2, -1e4, 0.0)
+    else:
+        mask = None
+    return q, k, v, mask
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("b,h,lq,lk,hd,mask_kind", [
+    (2, 12, 256, 256, 64, "add"),     # BERT-base self-attention, T = 256
+    (2, 4, 256, 256, 64, "bool"),     # text enhancer (4 heads of 64, phrase masks)
+    (2, 8, 900, 900, 32, "none"),     # decoder self-attention
+    (2, 8, 900, 256, 32, "keypad"),   # decoder text cross-attention
+    (1, 3, 77, 45, 32, "bool"),       # ragged
+])
+def test_attention_fwd_bwd(dtype, tol, b, h, lq, lk, hd, mask_kind):
+    from gdino_amd.attn import AttnFunction
+    from oracle.blocks import attention_ref
+    q, k, v, mask = _attn_inputs(b, h, lq, lk, hd, mask_kind, dtype, seed=lq + lk)
+    scale = hd ** -0.5
+    ref_in = [t.double().requires_grad_(True) for t in (q, k, v)]
+    md = None if mask is None else (mask if mask.dtype == torch.bool else mask.double())
+    ref = attention_ref(*ref_in, md, scale)
+    grad = torch.randn(ref.shape, generator=torch.Generator().manual_seed(2)).to(dtype)
+    ref.backward(grad.double())
+    dev = [t.to(DEV).requires_grad_(True) for t in (q, k, v)]
+    out = AttnFunction.apply(*dev, None if mask is None else mask.to(DEV), scale)
+    out.backward(grad.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref.detach()) < tol
+    for name, mine, r in zip(("dq", "dk", "dv"), dev, ref_in):
+        assert _rel(mine.grad.cpu(), r.grad) < tol * 3, name
+
+
+def test_attention_op_routes_to_hip_and_falls_back():
+    """kernels.attention runs the HIP kernel for head_dim 32/64 without
+    dropout and PyTorch SDPA otherwise (head_dim 256: BiAttention-sized)."""
+    from gdino_amd import attn, kernels
+    from oracle.blocks import attention_ref
+    q, k, v, mask = _attn_inputs(2, 4, 100, 60, 64, "bool", torch.float32)
+    assert attn.supported(q, k, v, 0.0) and not attn.supported(q, k, v, 0.1)
+    out = kernels.attention(q.to(DEV), k.to(DEV), v.to(DEV), mask.to(DEV))
+    assert _rel(out.cpu(), attention_ref(q.double(), k.double(), v.double(), mask)) < 1e-3
+    q2, k2, v2, _ = _attn_inputs(1, 2, 40, 30, 256, "none", torch.float32)
+    assert not attn.supported(q2, k2, v2, 0.0)
+    out2 = kernels.attention(q2.to(DEV), k2.to(DEV), v2.to(DEV))
+    assert _rel(out2.cpu(), attention_ref(q2.double(), k2.double(), v2.double())) < 1e-3
