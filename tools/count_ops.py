@@ -95,7 +95,7 @@ def main():
     # the GPU; the oracle restatements' own ops (forward and their autograd
     # backward) are not counted
     import models.GroundingDINO.ms_deform_attn as msda_mod
-    from oracle.blocks import bi_attention_ref
+    from oracle.blocks import attention_ref, bi_attention_ref, window_attention_packed_ref
 
     def counted(fn, tag):
         class Op(torch.autograd.Function):
@@ -142,6 +142,14 @@ def main():
     def counted_bi(q, k, vv, vl, pv=None, pl=None, p=0.0):
         return bi_op(q, k, vv, vl, pv, pl)
 
+    win_op = counted(lambda qkv, t, r, m, sc: window_attention_packed_ref(qkv.float(), t.float(), r, m, sc)
+                     .to(qkv.dtype), "gd.window_attn")
+    attn_op = counted(lambda q, k, v, m, sc: attention_ref(q.float(), k.float(), v.float(), m, sc).to(q.dtype),
+                      "gd.attn")
+
+    def counted_attn(q, k, v, m=None, sc=None, p=0.0):
+        return attn_op(q, k, v, m, sc)
+
     prev = msda_mod.MSDeformAttnFunction
     msda_mod.MSDeformAttnFunction = CountedMSDA
     amp = None if a.no_autocast else torch.bfloat16
@@ -168,7 +176,8 @@ def main():
         c.paused -= 1
 
     try:
-        with kernels.override("bi_attention", counted_bi):
+        with kernels.override("bi_attention", counted_bi), \
+                kernels.override("window_attention_packed", win_op), kernels.override("attention", counted_attn):
             step(Counter())  # warm-up (caches)
             with counter:
                 step(counter)
