@@ -176,19 +176,23 @@ gd_status gd_window_attn_backward(gd_dtype dtype, const void* qkv, const float* 
  * dtype F32 or BF16, head_dim 32 or 64, Lq, Lk > 0, B*H < 65536.
  * lse [B, H, Lq] F32: per-row log-sum-exp (+inf for a row with every key
  * masked, whose output is 0), input of the backward.
+ * dropout_p in [0, 1): attention-probability dropout after the softmax
+ * normaliser; element (b, h, q, k) is dropped when
+ * lowbias32(k*0x9E3779B1 ^ q*0x85EBCA77 ^ (b*H+h)*0xC2B2AE3D ^ seed)
+ * < dropout_p * 2^32 (the backward must get the same seed).
  */
 gd_status gd_attn_forward(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,
                           const int64_t* q_strides, const void* k, const int64_t* k_strides,
                           const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
-                          const int64_t* mask_strides, float scale, void* out,
-                          const int64_t* out_strides, float* lse, gd_stream_t stream);
+                          const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                          void* out, const int64_t* out_strides, float* lse, gd_stream_t stream);
 /* dsum: [B, H, Lq] F32 workspace (rowsum(dO . O)); grad_q / grad_k / grad_v
  * are fully written. */
 gd_status gd_attn_backward(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,
                            const int64_t* q_strides, const void* k, const int64_t* k_strides,
                            const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
-                           const int64_t* mask_strides, float scale, const void* out,
-                           const int64_t* out_strides, const void* grad_out,
+                           const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                           const void* out, const int64_t* out_strides, const void* grad_out,
                            const int64_t* grad_out_strides, const float* lse, float* dsum,
                            void* grad_q, const int64_t* grad_q_strides, void* grad_k,
                            const int64_t* grad_k_strides, void* grad_v,

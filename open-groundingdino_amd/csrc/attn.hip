@@ -20,7 +20,8 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 gd_status fill(AttnArgs& a, gd_dtype dt, int B, int H, int Lq, int Lk, int hd, const void* q, const int64_t* qs,
                const void* k, const int64_t* ks, const void* v, const int64_t* vs, const void* mask, int mask_kind,
-               const int64_t* ms, float scale) {
+               const int64_t* ms, float scale, float dropout_p, uint32_t seed) {
+  GD_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f, "attn: dropout_p %g outside [0, 1)", double(dropout_p));
   GD_REQUIRE(dt == GD_F32 || dt == GD_BF16, "attn: dtype %d not supported (F32, BF16)", int(dt));
   GD_REQUIRE(B >= 0 && H > 0 && Lq > 0 && Lk > 0, "attn: bad sizes B=%d H=%d Lq=%d Lk=%d", B, H, Lq, Lk);
   GD_REQUIRE(int64_t(B) * H < 65536, "attn: B*H=%lld exceeds the grid's y dimension", (long long)B * H);
@@ -49,6 +50,10 @@ gd_status fill(AttnArgs& a, gd_dtype dt, int B, int H, int Lq, int Lk, int hd, c
   a.Lq = Lq;
   a.Lk = Lk;
   a.scale = scale;
+  a.dropout = dropout_p > 0.f;
+  a.drop_thresh = uint32_t(fmin(double(dropout_p) * 4294967296.0, 4294967295.0));
+  a.drop_scale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
+  a.seed = seed;
   return GD_OK;
 }
 
@@ -77,11 +82,11 @@ using namespace gd;
 extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
                                      const int64_t* q_strides, const void* k, const int64_t* k_strides,
                                      const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
-                                     const int64_t* mask_strides, float scale, void* out,
-                                     const int64_t* out_strides, float* lse, gd_stream_t stream) {
+                                     const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                                     void* out, const int64_t* out_strides, float* lse, gd_stream_t stream) {
   AttnArgs a;
   GD_RET(fill(a, dt, B, H, Lq, Lk, head_dim, q, q_strides, k, k_strides, v, v_strides, mask, mask_kind,
-              mask_strides, scale));
+              mask_strides, scale, dropout_p, seed));
   if (B == 0) return GD_OK;
   GD_RET(take_strides(a.os, out_strides, out, dt, "out"));
   GD_REQUIRE(lse, "attn: null lse");
@@ -103,7 +108,8 @@ extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, 
 extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
                                       const int64_t* q_strides, const void* k, const int64_t* k_strides,
                                       const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
-                                      const int64_t* mask_strides, float scale, const void* out,
+                                      const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                                      const void* out,
                                       const int64_t* out_strides, const void* grad_out,
                                       const int64_t* grad_out_strides, const float* lse, float* dsum,
                                       void* grad_q, const int64_t* grad_q_strides, void* grad_k,
@@ -111,7 +117,7 @@ extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk,
                                       gd_stream_t stream) {
   AttnArgs a;
   GD_RET(fill(a, dt, B, H, Lq, Lk, head_dim, q, q_strides, k, k_strides, v, v_strides, mask, mask_kind,
-              mask_strides, scale));
+              mask_strides, scale, dropout_p, seed));
   if (B == 0) return GD_OK;
   GD_RET(take_strides(a.os, out_strides, out, dt, "out"));
   GD_RET(take_strides(a.gs, grad_out_strides, grad_out, dt, "grad_out"));

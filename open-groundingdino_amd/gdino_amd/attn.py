@@ -17,9 +17,12 @@ q [B, H, Lq, hd], k / v [B, H, Lk, hd] are read in place through their
 attn_mask is a bool keep-mask (True = attend) or an additive float mask
 broadcastable to [B, H, Lq, Lk].  The output is stored [B, Lq, H, hd] (what
 BERT's and the MHA's output projections read) and returned as the
-[B, H, Lq, hd] view.  The kernels cover head_dim 32 / 64 in fp32 and bf16
-without attention-probability dropout; anything else uses PyTorch SDPA
-(ROCm flash / mem-efficient kernels).  CPU tensors raise.
+[B, H, Lq, hd] view.  The kernels cover head_dim 32 / 64 in fp32 and bf16,
+with attention-probability dropout (BERT's attention dropout 0.1 in training)
+drawn from a counter-based hash of (seed, b*H+h, q, k) that the backward
+regenerates -- the same distribution as torch's dropout, not its RNG stream.
+Anything else uses PyTorch SDPA (ROCm flash / mem-efficient kernels).  CPU
+tensors raise.
 """
 from __future__ import annotations
 
@@ -31,8 +34,9 @@ import torch.nn.functional as F
 from . import _lib, kernels
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
-_lib.register("gd_attn_forward", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _p, _p, _p, _p])
-_lib.register("gd_attn_backward", [_i] * 6 + [_p] * 7 + [_i, _p, _f] + [_p] * 13)
+_u32 = ctypes.c_uint32
+_lib.register("gd_attn_forward", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u32, _p, _p, _p, _p])
+_lib.register("gd_attn_backward", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u32] + [_p] * 13)
 
 
 def _st3(t):
@@ -66,14 +70,14 @@ def _mask_args(mask, b, h, lq, lk):
 
 def supported(q, k, v, dropout_p) -> bool:
     hd = q.shape[-1]
-    return (dropout_p == 0.0 and q.dtype in (torch.float32, torch.bfloat16) and q.dtype == k.dtype == v.dtype
+    return (0.0 <= dropout_p < 1.0 and q.dtype in (torch.float32, torch.bfloat16) and q.dtype == k.dtype == v.dtype
             and hd in (32, 64) and k.shape[-1] == hd and v.shape[-1] == hd and q.shape[2] > 0 and k.shape[2] > 0
             and q.shape[0] * q.shape[1] < 65536)
 
 
 class AttnFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, mask, scale):
+    def forward(ctx, q, k, v, mask, scale, dropout_p=0.0, seed=0):
         _lib.require_device(q, k, v, mask, what="attention")
         q, k, v = _rows(q), _rows(k), _rows(v)
         b, h, lq, hd = q.shape
@@ -82,10 +86,11 @@ class AttnFunction(torch.autograd.Function):
         out = torch.empty(b, lq, h, hd, dtype=q.dtype, device=q.device).transpose(1, 2)
         lse = torch.empty(b, h, lq, dtype=torch.float32, device=q.device)
         _lib.call("gd_attn_forward", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
-                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), kind, ms, float(scale), out.data_ptr(), _st3(out),
-                  lse.data_ptr(), _lib.stream_of(q))
+                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), kind, ms, float(scale), float(dropout_p), int(seed),
+                  out.data_ptr(), _st3(out), lse.data_ptr(), _lib.stream_of(q))
         ctx.save_for_backward(q, k, v, m, out, lse)
         ctx.kind, ctx.ms, ctx.scale = kind, tuple(ms) if ms is not None else None, float(scale)
+        ctx.dropout_p, ctx.seed = float(dropout_p), int(seed)
         return out
 
     @staticmethod
@@ -99,10 +104,10 @@ class AttnFunction(torch.autograd.Function):
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         dq, dk, dv = _rows(dq), _rows(dk), _rows(dv)
         _lib.call("gd_attn_backward", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
-                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), ctx.kind, ms, ctx.scale, out.data_ptr(), _st3(out),
-                  dout.data_ptr(), _st3(dout), lse.data_ptr(), dsum.data_ptr(), dq.data_ptr(), _st3(dq),
-                  dk.data_ptr(), _st3(dk), dv.data_ptr(), _st3(dv), _lib.stream_of(q))
-        return dq, dk, dv, None, None
+                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), ctx.kind, ms, ctx.scale, ctx.dropout_p, ctx.seed,
+                  out.data_ptr(), _st3(out), dout.data_ptr(), _st3(dout), lse.data_ptr(), dsum.data_ptr(),
+                  dq.data_ptr(), _st3(dq), dk.data_ptr(), _st3(dk), dv.data_ptr(), _st3(dv), _lib.stream_of(q))
+        return dq, dk, dv, None, None, None, None
 
 
 def attention_hip(q, k, v, attn_mask=None, scale=None, dropout_p=0.0):
@@ -110,6 +115,11 @@ def attention_hip(q, k, v, attn_mask=None, scale=None, dropout_p=0.0):
     if not supported(q, k, v, dropout_p):
         return F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=dropout_p, scale=scale)
     scale = q.shape[-1] ** -0.5 if scale is None else scale
+    if dropout_p > 0.0:
+        # per-call mask seed from torch's (CPU) generator: torch.manual_seed
+        # reproduces it, no device sync
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        return AttnFunction.apply(q, k, v, attn_mask, scale, dropout_p, seed)
     return AttnFunction.apply(q, k, v, attn_mask, scale)
 
 

@@ -36,8 +36,9 @@ def lib():
         _LIB.gd_window_attn_forward.argtypes = [_i, _p, _p, _p, _p] + [_i] * 5 + [ctypes.c_float, _p, _p, _p]
         _LIB.gd_window_attn_backward.argtypes = ([_i, _p, _p, _p, _p, _p, _p, _p] + [_i] * 5 +
                                                  [ctypes.c_float, _p, _p, _p])
-        _LIB.gd_attn_forward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, ctypes.c_float, _p, _p, _p, _p]
-        _LIB.gd_attn_backward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, ctypes.c_float] + [_p] * 13
+        _f, _u = ctypes.c_float, ctypes.c_uint32
+        _LIB.gd_attn_forward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u, _p, _p, _p, _p]
+        _LIB.gd_attn_backward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u] + [_p] * 13
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -160,7 +161,7 @@ def _mask_args(mask):
     return m, kind, (ctypes.c_int64 * 3)(*st)
 
 
-def attn_forward(q, k, v, mask, scale):
+def attn_forward(q, k, v, mask, scale, dropout_p=0.0, seed=0):
     """q [B,H,Lq,hd], k/v [B,H,Lk,hd] (any (b,h,l) strides, contiguous hd)
     -> out [B,H,Lq,hd] (stored [B,Lq,H,hd]), lse [B,H,Lq]"""
     B, H, Lq, hd = q.shape
@@ -169,11 +170,11 @@ def attn_forward(q, k, v, mask, scale):
     out = torch.empty(B, Lq, H, hd, dtype=q.dtype).transpose(1, 2)
     lse = torch.empty(B, H, Lq, dtype=torch.float32)
     _check(lib().gd_attn_forward(_code(q), B, H, Lq, Lk, hd, _ptr(q), _st3(q), _ptr(k), _st3(k), _ptr(v), _st3(v),
-                                 _ptr(m), kind, ms, scale, _ptr(out), _st3(out), _ptr(lse), None))
+                                 _ptr(m), kind, ms, scale, dropout_p, seed, _ptr(out), _st3(out), _ptr(lse), None))
     return out, lse
 
 
-def attn_backward(q, k, v, mask, scale, out, lse, grad_out):
+def attn_backward(q, k, v, mask, scale, out, lse, grad_out, dropout_p=0.0, seed=0):
     B, H, Lq, hd = q.shape
     Lk = k.shape[2]
     m, kind, ms = _mask_args(mask)
@@ -182,10 +183,30 @@ def attn_backward(q, k, v, mask, scale, out, lse, grad_out):
     dk = torch.full_like(k, float("nan"))
     dv = torch.full_like(v, float("nan"))
     _check(lib().gd_attn_backward(_code(q), B, H, Lq, Lk, hd, _ptr(q), _st3(q), _ptr(k), _st3(k), _ptr(v), _st3(v),
-                                  _ptr(m), kind, ms, scale, _ptr(out), _st3(out), _ptr(grad_out), _st3(grad_out),
+                                  _ptr(m), kind, ms, scale, dropout_p, seed, _ptr(out), _st3(out), _ptr(grad_out),
+                                  _st3(grad_out),
                                   _ptr(lse), _ptr(dsum), _ptr(dq), _st3(dq), _ptr(dk), _st3(dk), _ptr(dv), _st3(dv),
                                   None))
     return dq, dk, dv
+
+
+def attn_dropout_keep(B, H, Lq, Lk, p, seed):
+    """The kernels' dropout mask (include/gdino_amd.h, gd_attn_forward):
+    keep[b, h, q, k] = lowbias32(k*0x9E3779B1 ^ q*0x85EBCA77 ^ (b*H+h)*0xC2B2AE3D
+    ^ seed) >= p * 2^32, restated in numpy uint32 arithmetic."""
+    M = np.uint32(0xFFFFFFFF)
+    k = np.arange(Lk, dtype=np.uint64)[None, None, :]
+    q = np.arange(Lq, dtype=np.uint64)[None, :, None]
+    bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
+    x = ((k * 0x9E3779B1) & 0xFFFFFFFF) ^ ((q * 0x85EBCA77) & 0xFFFFFFFF) ^ ((bh * 0xC2B2AE3D) & 0xFFFFFFFF) ^ seed
+    x = x.astype(np.uint64)
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    thresh = min(int(p * 4294967296.0), int(M))
+    return torch.from_numpy((x >= thresh).reshape(B, H, Lq, Lk))
 
 
 def rel_err(a, b):

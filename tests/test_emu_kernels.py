@@ -343,3 +343,25 @@ def test_emulated_attention_fully_masked_rows_are_zero():
     dq, dk, dv = E.attn_backward(q, k, v, mask, scale, out, lse, grad)
     assert torch.isfinite(dq).all() and torch.isfinite(dk).all() and torch.isfinite(dv).all()
     assert torch.equal(dq[:, :, 3], torch.zeros_like(dq[:, :, 3]))
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
+def test_emulated_attention_dropout(dtype, tol):
+    """Attention-probability dropout (BERT's 0.1 in training): output and
+    gradients equal the reference math with the kernels' counter-based mask
+    Z applied after the softmax normaliser, O = (softmax(S) . Z / (1-p)) V;
+    the backward regenerates Z from the same seed."""
+    p, seed = 0.25, 12345
+    B, H, Lq, Lk, hd = 2, 2, 70, 90, 64
+    q, k, v, mask, scale, grad = _attn_case(B, H, Lq, Lk, hd, "add", dtype, seed=7, layout="blh")
+    out, lse = E.attn_forward(q, k, v, mask, scale, p, seed)
+    keep = E.attn_dropout_keep(B, H, Lq, Lk, p, seed)
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
+    prob = torch.softmax((qd @ kd.transpose(-1, -2)) * scale + mask.double(), -1)
+    ref = (prob * keep / (1 - p)) @ vd
+    assert E.rel_err(out.double(), ref.detach()) < tol
+    ref.backward(grad.double())
+    dq, dk, dv = E.attn_backward(q, k, v, mask, scale, out, lse, grad, p, seed)
+    for name, mine, r in (("dq", dq, qd.grad), ("dk", dk, kd.grad), ("dv", dv, vd.grad)):
+        assert E.rel_err(mine.double(), r) < tol * 2, name

@@ -173,15 +173,38 @@ def test_attention_fwd_bwd(dtype, tol, b, h, lq, lk, hd, mask_kind):
 
 
 def test_attention_op_routes_to_hip_and_falls_back():
-    """kernels.attention runs the HIP kernel for head_dim 32/64 without
-    dropout and PyTorch SDPA otherwise (head_dim 256: BiAttention-sized)."""
+    """kernels.attention runs the HIP kernel for head_dim 32/64 and PyTorch
+    SDPA otherwise (head_dim 256: BiAttention-sized)."""
     from gdino_amd import attn, kernels
     from oracle.blocks import attention_ref
     q, k, v, mask = _attn_inputs(2, 4, 100, 60, 64, "bool", torch.float32)
-    assert attn.supported(q, k, v, 0.0) and not attn.supported(q, k, v, 0.1)
+    assert attn.supported(q, k, v, 0.0) and attn.supported(q, k, v, 0.1)
     out = kernels.attention(q.to(DEV), k.to(DEV), v.to(DEV), mask.to(DEV))
     assert _rel(out.cpu(), attention_ref(q.double(), k.double(), v.double(), mask)) < 1e-3
     q2, k2, v2, _ = _attn_inputs(1, 2, 40, 30, 256, "none", torch.float32)
     assert not attn.supported(q2, k2, v2, 0.0)
     out2 = kernels.attention(q2.to(DEV), k2.to(DEV), v2.to(DEV))
     assert _rel(out2.cpu(), attention_ref(q2.double(), k2.double(), v2.double())) < 1e-3
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+def test_attention_dropout_matches_reference_with_the_kernel_mask(dtype, tol):
+    """BERT-shaped attention with dropout 0.1 (training): the reference math
+    with the kernels' counter-based keep-mask (tests/emu_lib.attn_dropout_keep)."""
+    from emu_lib import attn_dropout_keep
+    from gdino_amd.attn import AttnFunction
+    b, h, lq, lk, hd, p, seed = 2, 12, 256, 256, 64, 0.1, 987
+    q, k, v, mask = _attn_inputs(b, h, lq, lk, hd, "add", dtype, seed=5)
+    keep = attn_dropout_keep(b, h, lq, lk, p, seed)
+    ref_in = [t.double().requires_grad_(True) for t in (q, k, v)]
+    prob = torch.softmax(ref_in[0] @ ref_in[1].transpose(-1, -2) * hd ** -0.5 + mask.double(), -1)
+    ref = (prob * keep / (1 - p)) @ ref_in[2]
+    grad = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(dtype)
+    ref.backward(grad.double())
+    dev = [t.to(DEV).requires_grad_(True) for t in (q, k, v)]
+    out = AttnFunction.apply(*dev, mask.to(DEV), hd ** -0.5, p, seed)
+    out.backward(grad.to(DEV))
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref.detach()) < tol
+    for name, mine, r in zip(("dq", "dk", "dv"), dev, ref_in):
+        assert _rel(mine.grad.cpu(), r.grad) < tol * 3, name
