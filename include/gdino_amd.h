@@ -43,9 +43,12 @@
  *                        text enhancer's and the decoder's
  *                        nn.MultiheadAttention (transformer_vanilla.py:83,
  *                        transformer.py:839,844)
- *
- * Not (yet) in this ABI version — a hipBLASLt GEMM + masked_fill on the
- * device: ContrastiveEmbed (utils.py:242-273).
+ *   gd_contrastive_forward
+ *                     <- ContrastiveEmbed.forward (x . text^T, -inf on padded
+ *                        tokens, -inf right padding to max_text_len)
+ *                        models/GroundingDINO/utils.py:242-273, and the
+ *                        two-stage score enc_outputs_class_unselected.max(-1)
+ *                        models/GroundingDINO/transformer.py:292-296
  */
 #ifndef GDINO_AMD_H
 #define GDINO_AMD_H
@@ -197,6 +200,22 @@ gd_status gd_attn_backward(gd_dtype dtype, int B, int H, int Lq, int Lk, int hea
                            void* grad_q, const int64_t* grad_q_strides, void* grad_k,
                            const int64_t* grad_k_strides, void* grad_v,
                            const int64_t* grad_v_strides, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Contrastive text-alignment head (utils.py:242-273)                        */
+/* ------------------------------------------------------------------------ */
+/*
+ * x [B, Q, C] and text [B, T, C] (F32 or BF16) through host arrays of two
+ * element strides (b, row); rows contiguous and 16-byte aligned; C % 32 == 0.
+ * text_mask [B, T] uint8 (1 = real token), contiguous.  T <= Tout.
+ * logits [B, Q, Tout] F32 (or NULL): x . text^T, -inf where text_mask is 0
+ *        and for T <= t < Tout.
+ * rowmax [B, Q] F32 (or NULL): max over t of logits (-inf if no token).
+ */
+gd_status gd_contrastive_forward(gd_dtype dtype, const void* x, const int64_t* x_strides,
+                                 const void* text, const int64_t* text_strides,
+                                 const uint8_t* text_mask, int B, int Q, int T, int C, int Tout,
+                                 float* logits, float* rowmax, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

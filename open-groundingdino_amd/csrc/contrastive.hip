@@ -1,0 +1,128 @@
+// Contrastive text-alignment head for gfx950 (ContrastiveEmbed, reference
+// models/GroundingDINO/utils.py:242-273, used at groundingdino.py:332-337 and
+// for the two-stage selection transformer.py:292-296):
+//   logits[b, q, t] = x[b, q] . text[b, t]   (t < T and text_mask[b, t])
+//                   = -inf                   (masked token, or T <= t < Tout)
+// as one MFMA kernel writing the fp32 [B, Q, Tout] logits directly (the
+// reference: matmul, masked_fill, a -inf [B, Q, 256] fill and a slice copy),
+// and/or the row maxima max_t logits[b, q, t] -- the two-stage proposal score
+// (enc_outputs_class_unselected.max(-1)) without materialising the
+// [B, S, 256] logits of every image token.
+//
+// A wave owns 64 rows of x and walks the Tout columns in 64-token tiles;
+// every product is a 16x16x32 MFMA step with natural operands (mfma_frag.inc):
+// A = x rows (row q on the lane), B = text rows (column t on the lane), K = C.
+#include "gd_common.h"
+
+#include <cmath>
+
+namespace gd {
+namespace {
+#include "mfma_frag.inc"
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+contrastive_kernel(const T* __restrict__ x, int64_t xsb, int64_t xsq, const T* __restrict__ text, int64_t tsb,
+                   int64_t tst, const uint8_t* __restrict__ tmask, int Q, int Tn, int C, int Tout,
+                   float* __restrict__ out, float* __restrict__ rowmax) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y;
+  const int q0 = (blockIdx.x * 4 + wave) * 64;
+  if (q0 >= Q) return;  // no barriers in this kernel
+  const T* xb = x + b * xsb;
+  const T* tb = text + b * tsb;
+  float mx[4][4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[qt][r] = -INFINITY;
+
+  for (int t0 = 0; t0 < Tout; t0 += 64) {
+    gd_f32x4 acc[4][4];  // (row q0 + 16qt + 4g + r, token t0 + 16tt + c)
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) acc[qt][tt] = zero4();
+    if (t0 < Tn) {
+      for (int ch = 0; ch < C / 32; ++ch) {
+        WFrag<T> tf[4];
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const int t = t0 + 16 * tt + c;
+          tf[tt] = ld_frag<T>(tb + int64_t(t < Tn ? t : 0) * tst + 32 * ch + 8 * g, t < Tn);
+        }
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt) {
+          const int q = q0 + 16 * qt + c;
+          const WFrag<T> xf = ld_frag<T>(xb + int64_t(q < Q ? q : 0) * xsq + 32 * ch + 8 * g, q < Q);
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) acc[qt][tt] = wmma(xf, tf[tt], acc[qt][tt]);
+        }
+      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int t = t0 + 16 * tt + c;
+      const bool live = t < Tn && tmask[int64_t(b) * Tn + t] != 0;
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = q0 + 16 * qt + 4 * g + r;
+          const float v = live ? acc[qt][tt][r] : -INFINITY;
+          mx[qt][r] = fmaxf(mx[qt][r], v);
+          if (out && q < Q && t < Tout) out[(int64_t(b) * Q + q) * Tout + t] = v;
+        }
+    }
+  }
+  if (!rowmax) return;
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float m = mx[qt][r];
+      m = fmaxf(m, __shfl_xor(m, 1, 64));
+      m = fmaxf(m, __shfl_xor(m, 2, 64));
+      m = fmaxf(m, __shfl_xor(m, 4, 64));
+      m = fmaxf(m, __shfl_xor(m, 8, 64));
+      const int q = q0 + 16 * qt + 4 * g + r;
+      if (c == 0 && q < Q) rowmax[int64_t(b) * Q + q] = m;
+    }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+}  // namespace gd
+
+using namespace gd;
+
+extern "C" gd_status gd_contrastive_forward(gd_dtype dt, const void* x, const int64_t* x_strides, const void* text,
+                                           const int64_t* text_strides, const uint8_t* text_mask, int B, int Q,
+                                           int T, int C, int Tout, float* logits, float* rowmax,
+                                           gd_stream_t stream) {
+  GD_REQUIRE(dt == GD_F32 || dt == GD_BF16, "contrastive: dtype %d not supported (F32, BF16)", int(dt));
+  GD_REQUIRE(B >= 0 && Q >= 0 && T > 0 && C > 0 && C % 32 == 0 && Tout >= T && B < 65536,
+             "contrastive: bad sizes B=%d Q=%d T=%d C=%d (multiple of 32) Tout=%d (>= T)", B, Q, T, C, Tout);
+  GD_REQUIRE(logits || rowmax, "contrastive: neither logits nor rowmax requested");
+  if (B == 0 || Q == 0) return GD_OK;
+  GD_REQUIRE(x && text && text_mask && x_strides && text_strides, "contrastive: null pointer");
+  const int64_t align = 16 / (dt == GD_BF16 ? 2 : 4);
+  GD_REQUIRE(aligned16(x) && aligned16(text) && x_strides[0] % align == 0 && x_strides[1] % align == 0 &&
+                 text_strides[0] % align == 0 && text_strides[1] % align == 0,
+             "contrastive: x / text rows must be contiguous and 16-byte aligned");
+  hipStream_t s = as_hip(stream);
+  const dim3 grid(unsigned((Q + 255) / 256), unsigned(B));
+  if (dt == GD_BF16) {
+    hipLaunchKernelGGL((contrastive_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)x, x_strides[0],
+                       x_strides[1], (const uint16_t*)text, text_strides[0], text_strides[1], text_mask, Q, T, C,
+                       Tout, logits, rowmax);
+  } else {
+    hipLaunchKernelGGL((contrastive_kernel<float>), grid, dim3(256), 0, s, (const float*)x, x_strides[0],
+                       x_strides[1], (const float*)text, text_strides[0], text_strides[1], text_mask, Q, T, C, Tout,
+                       logits, rowmax);
+  }
+  GD_LAUNCH_CHECK("contrastive");
+  return GD_OK;
+}

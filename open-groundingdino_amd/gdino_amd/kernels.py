@@ -10,6 +10,8 @@ primitives, so that the implementation behind each op is one swap:
                      self-attn and text cross-attn): gdino_amd/attn.py
   bi_attention       BiMultiHeadAttention core   fuse_modules.py:162-246
   contrastive_logits ContrastiveEmbed            utils.py:242-273
+  contrastive_rowmax its max over tokens, the two-stage proposal score
+                     (transformer.py:292-296), without the [B, S, 256] logits
 
 ``IMPL[name]`` selects the implementation; ``"hip"`` entries are the
 hand-written gfx950 kernels of csrc/ (registered by their modules when the
@@ -138,7 +140,13 @@ def contrastive_logits(x, text, text_token_mask, max_text_len):
     return get("contrastive_logits")(x, text, text_token_mask, max_text_len)
 
 
+def contrastive_rowmax(x, text, text_token_mask):
+    """max_t contrastive_logits(x, text, mask)[..., t] -> [B, Q] fp32, no grad."""
+    return get("contrastive_rowmax")(x, text, text_token_mask)
+
+
 # HIP implementations register themselves as the defaults for CUDA tensors.
 from . import biattn  # noqa: E402,F401
 from . import wattn  # noqa: E402,F401
 from . import attn  # noqa: E402,F401
+from . import contrastive  # noqa: E402,F401

@@ -21,6 +21,7 @@ import torch
 import torch.utils.checkpoint as checkpoint
 from torch import Tensor, nn
 
+from gdino_amd import kernels
 from gdino_amd.mha import MultiheadAttention
 from gdino_amd.misc import device_const, inverse_sigmoid
 
@@ -154,8 +155,11 @@ class Transformer(nn.Module):
         if self.two_stage_type == "standard":
             output_memory, output_proposals = gen_encoder_output_proposals(memory, mask_flatten, shapes_list)
             output_memory = self.enc_output_norm(self.enc_output(output_memory))
-            enc_cls = self.enc_out_class_embed(output_memory, text_dict)
-            topk_logits = enc_cls.max(-1)[0]
+            # enc_out_class_embed(output_memory, text_dict).max(-1)[0]
+            # (reference :292-293), without the [bs, S, 256] logits: only the
+            # top-k indices are used (gdino_amd/contrastive.py)
+            topk_logits = kernels.contrastive_rowmax(output_memory, text_dict["encoded_text"],
+                                                     text_dict["text_token_mask"])
             enc_coord = self.enc_out_bbox_embed(output_memory) + output_proposals
             topk_proposals = torch.topk(topk_logits, self.num_queries, dim=1)[1]  # [bs, nq]
             idx4 = topk_proposals.unsqueeze(-1).expand(-1, -1, 4)

@@ -39,6 +39,7 @@ def lib():
         _f, _u = ctypes.c_float, ctypes.c_uint32
         _LIB.gd_attn_forward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u, _p, _p, _p, _p]
         _LIB.gd_attn_backward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u] + [_p] * 13
+        _LIB.gd_contrastive_forward.argtypes = [_i] + [_p] * 5 + [_i] * 5 + [_p, _p, _p]
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -188,6 +189,20 @@ def attn_backward(q, k, v, mask, scale, out, lse, grad_out, dropout_p=0.0, seed=
                                   _ptr(lse), _ptr(dsum), _ptr(dq), _st3(dq), _ptr(dk), _st3(dk), _ptr(dv), _st3(dv),
                                   None))
     return dq, dk, dv
+
+
+def contrastive_forward(x, text, mask, tout, want_logits=True, want_rowmax=True):
+    """x [B, Q, C], text [B, T, C] (f32/bf16), mask [B, T] bool keep ->
+    (logits [B, Q, tout] f32 or None, rowmax [B, Q] f32 or None)"""
+    B, Q, C = x.shape
+    T = text.shape[1]
+    keep = mask.to(torch.uint8).contiguous()
+    logits = torch.full((B, Q, tout), float("nan")) if want_logits else None
+    rowmax = torch.full((B, Q), float("nan")) if want_rowmax else None
+    _check(lib().gd_contrastive_forward(_code(x), _ptr(x), (ctypes.c_int64 * 2)(*x.stride()[:2]), _ptr(text),
+                                        (ctypes.c_int64 * 2)(*text.stride()[:2]), _ptr(keep), B, Q, T, C, tout,
+                                        _ptr(logits), _ptr(rowmax), None))
+    return logits, rowmax
 
 
 def attn_dropout_keep(B, H, Lq, Lk, p, seed):

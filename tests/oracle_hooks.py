@@ -1,5 +1,5 @@
 """Test-only: run the model's host logic on CPU by routing the HIP-only ops
-(MSDA, BiAttention softmax, window attention, masked attention) to their oracle restatements.  The product raises on CPU tensors; this hook
+(MSDA, BiAttention softmax, window attention, masked attention, contrastive head) to their oracle restatements.  The product raises on CPU tensors; this hook
 is the only way CPU tests execute MSDA."""
 import contextlib
 
@@ -17,7 +17,7 @@ def oracle_msda():
     """Route every HIP-only op to its oracle restatement (CPU tests)."""
     import models.GroundingDINO.ms_deform_attn as mod
     from gdino_amd import kernels
-    from oracle.blocks import attention_ref, bi_attention_ref, window_attention_packed_ref
+    from oracle.blocks import attention_ref, bi_attention_ref, contrastive_ref, window_attention_packed_ref
 
     prev = mod.MSDeformAttnFunction
     mod.MSDeformAttnFunction = _OracleMSDA
@@ -26,7 +26,10 @@ def oracle_msda():
                               bi_attention_ref(q, k, vv, vl, pv, pl)), \
                 kernels.override("window_attention_packed", window_attention_packed_ref), \
                 kernels.override("attention", lambda q, k, v, m=None, sc=None, p=0.0:
-                                 attention_ref(q, k, v, m, sc)):
+                                 attention_ref(q, k, v, m, sc)), \
+                kernels.override("contrastive_logits", contrastive_ref), \
+                kernels.override("contrastive_rowmax", lambda x, t, m:
+                                 contrastive_ref(x, t, m, t.shape[1]).detach().max(-1)[0]):
             yield
     finally:
         mod.MSDeformAttnFunction = prev

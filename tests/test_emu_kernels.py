@@ -202,6 +202,7 @@ t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)
 t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
 t.test_emulated_attention(2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh")
 t.test_emulated_attention(1, 1, 33, 300, 32, "add", torch.float32, 1e-5, "blh")
+t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
 print("asan-clean")
 """
 
@@ -365,3 +366,26 @@ def test_emulated_attention_dropout(dtype, tol):
     dq, dk, dv = E.attn_backward(q, k, v, mask, scale, out, lse, grad, p, seed)
     for name, mine, r in (("dq", dq, qd.grad), ("dk", dk, kd.grad), ("dv", dv, vd.grad)):
         assert E.rel_err(mine.double(), r) < tol * 2, name
+
+
+# --------------------------------------------------- contrastive head
+@pytest.mark.parametrize("B,Q,T,C,tout,dtype,tol", [
+    (2, 100, 37, 64, 256, torch.float32, 1e-5),    # padded to max_text_len
+    (1, 70, 256, 256, 256, torch.float32, 1e-5),   # full caption, hidden 256
+    (2, 130, 90, 256, 256, torch.bfloat16, 1e-5),  # bf16-exact inputs, fp32 accumulation
+])
+def test_emulated_contrastive(B, Q, T, C, tout, dtype, tol):
+    from oracle.blocks import contrastive_ref
+    g = torch.Generator().manual_seed(Q + T)
+    x = torch.randn(B, Q, C, generator=g).to(dtype)
+    text = torch.randn(B, T, C, generator=g).to(dtype)
+    mask = torch.rand(B, T, generator=g) < 0.8
+    mask[:, 0] = True
+    logits, rowmax = E.contrastive_forward(x, text, mask, tout)
+    ref = contrastive_ref(x.double(), text.double(), mask, tout).double()
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isfinite(logits), fin) and (logits[~fin] == float("-inf")).all()
+    assert E.rel_err(logits[fin], ref[fin]) < tol
+    assert E.rel_err(rowmax, ref.max(-1)[0]) < tol
+    _, only_max = E.contrastive_forward(x, text, mask, T, want_logits=False)
+    assert torch.equal(only_max, rowmax)

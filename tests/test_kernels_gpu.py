@@ -208,3 +208,34 @@ def test_attention_dropout_matches_reference_with_the_kernel_mask(dtype, tol):
     assert _rel(out.cpu(), ref.detach()) < tol
     for name, mine, r in zip(("dq", "dk", "dv"), dev, ref_in):
         assert _rel(mine.grad.cpu(), r.grad) < tol * 3, name
+
+
+# ------------------------------------------------ contrastive head (HIP)
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("b,q,t", [(2, 900, 256), (2, 900, 37), (2, 22223, 200)])
+def test_contrastive_logits_and_rowmax(dtype, tol, b, q, t):
+    """Decoder heads (900 queries) and the two-stage encoder scores (22 223
+    image tokens at 800x1333): logits, -inf pad / mask structure, gradients,
+    and the row max used for the top-900 selection."""
+    from gdino_amd.contrastive import ContrastiveFunction, contrastive_rowmax_hip
+    from oracle.blocks import contrastive_ref
+    g = torch.Generator().manual_seed(q + t)
+    x = torch.randn(b, q, 256, generator=g).to(dtype)
+    text = torch.randn(b, t, 256, generator=g).to(dtype)
+    mask = torch.rand(b, t, generator=g) < 0.8
+    mask[:, 0] = True
+    xd, td = x.double().requires_grad_(True), text.double().requires_grad_(True)
+    ref = contrastive_ref(xd, td, mask, 256)
+    fin = torch.isfinite(ref.detach())
+    xg, tg = x.to(DEV).requires_grad_(True), text.to(DEV).requires_grad_(True)
+    out = ContrastiveFunction.apply(xg, tg, mask.to(DEV), 256)
+    gout = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
+    out.backward(gout.to(DEV))
+    (ref.masked_fill(~fin, 0.0) * gout.double()).sum().backward()
+    o = out.detach().cpu()
+    assert torch.equal(torch.isfinite(o), fin) and (o[~fin] == float("-inf")).all()
+    assert _rel(o[fin], ref.detach()[fin]) < tol
+    assert _rel(xg.grad.cpu(), xd.grad) < tol * 3
+    assert _rel(tg.grad.cpu(), td.grad) < tol * 3
+    rm = contrastive_rowmax_hip(x.to(DEV), text.to(DEV), mask.to(DEV)).cpu()
+    assert _rel(rm, ref.detach().max(-1)[0]) < tol

@@ -138,7 +138,11 @@ def test_window_attention_and_attention_and_contrastive():
     x, txt = torch.randn(2, 50, 32, generator=g), torch.randn(2, 11, 32, generator=g)
     tm = torch.ones(2, 11, dtype=torch.bool)
     tm[1, 7:] = False
-    torch.testing.assert_close(kernels.contrastive_logits(x, txt, tm, 256), contrastive_ref(x, txt, tm, 256))
+    torch.testing.assert_close(kernels._contrastive_torch(x, txt, tm, 256), contrastive_ref(x, txt, tm, 256))
+    from gdino_amd.contrastive import contrastive_rowmax_torch
+    torch.testing.assert_close(contrastive_rowmax_torch(x, txt, tm), contrastive_ref(x, txt, tm, 256).max(-1)[0])
+    with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
+        kernels.contrastive_logits(x, txt, tm, 256)
 
 
 def test_mha_matches_torch_multihead_attention():
