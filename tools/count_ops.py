@@ -95,7 +95,7 @@ def main():
     # the GPU; the oracle restatements' own ops (forward and their autograd
     # backward) are not counted
     import models.GroundingDINO.ms_deform_attn as msda_mod
-    from oracle.blocks import attention_ref, bi_attention_ref, window_attention_packed_ref
+    from oracle.blocks import attention_ref, bi_attention_ref, contrastive_ref, window_attention_packed_ref
 
     def counted(fn, tag):
         class Op(torch.autograd.Function):
@@ -150,6 +150,17 @@ def main():
     def counted_attn(q, k, v, m=None, sc=None, p=0.0):
         return attn_op(q, k, v, m, sc)
 
+    con_op = counted(lambda x, t, m, n: contrastive_ref(x.float(), t.float(), m, n), "gd.contrastive")
+
+    def counted_rowmax(x, t, m):
+        counter.counts["gd.contrastive_rowmax"] += 1
+        counter.paused += 1
+        try:
+            with torch.no_grad():
+                return contrastive_ref(x.float(), t.float(), m, t.shape[1]).max(-1)[0]
+        finally:
+            counter.paused -= 1
+
     prev = msda_mod.MSDeformAttnFunction
     msda_mod.MSDeformAttnFunction = CountedMSDA
     amp = None if a.no_autocast else torch.bfloat16
@@ -177,7 +188,8 @@ def main():
 
     try:
         with kernels.override("bi_attention", counted_bi), \
-                kernels.override("window_attention_packed", win_op), kernels.override("attention", counted_attn):
+                kernels.override("window_attention_packed", win_op), kernels.override("attention", counted_attn), \
+                kernels.override("contrastive_logits", con_op), kernels.override("contrastive_rowmax", counted_rowmax):
             step(Counter())  # warm-up (caches)
             with counter:
                 step(counter)
