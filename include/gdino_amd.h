@@ -21,6 +21,9 @@
  *                        models/GroundingDINO/ops/src/vision.cpp:15,
  *                        ops/src/ms_deform_attn.h:41-61,
  *                        ops/src/cuda/ms_deform_attn_cuda.cu:83-153
+ *   gd_msda_backward_geom  the same, given a host copy of the level shapes
+ *                        (enables the pixel-block tiling of the encoder
+ *                        backward; no reference counterpart)
  *   gd_runtime_info   <- get_cuda_version
  *                        models/GroundingDINO/csrc/vision.cpp:11-51,
  *                        models/GroundingDINO/csrc/cuda_version.cu
@@ -118,6 +121,21 @@ gd_status gd_msda_backward(gd_dtype value_dtype, const void* value,
                            int num_levels, int num_query, int num_point,
                            void* grad_value, void* grad_sampling_loc,
                            void* grad_attn_weight, gd_stream_t stream);
+/* gd_msda_backward with a HOST copy of spatial_shapes ([num_levels][2]
+ * int64, or NULL = gd_msda_backward).  When the levels tile the queries
+ * exactly (num_query == spatial_size == sum H*W: the encoder), the backward
+ * takes 4 x 8 pixel blocks of each level as its LDS pre-aggregation tiles
+ * instead of 32 consecutive queries; results are the same sums. */
+gd_status gd_msda_backward_geom(gd_dtype value_dtype, const void* value,
+                                const int64_t* spatial_shapes,
+                                const int64_t* level_start_index,
+                                const void* sampling_loc, const void* attn_weight,
+                                const void* grad_output, int batch,
+                                int spatial_size, int num_heads, int channels,
+                                int num_levels, int num_query, int num_point,
+                                void* grad_value, void* grad_sampling_loc,
+                                void* grad_attn_weight, const int64_t* spatial_shapes_host,
+                                gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* BiAttention bidirectional softmax (fuse_modules.py:174-217)               */

@@ -125,13 +125,13 @@ extern "C" gd_status gd_msda_forward(gd_dtype dt, const void* value,
   return GD_OK;
 }
 
-extern "C" gd_status gd_msda_backward(gd_dtype dt, const void* value,
-                                      const int64_t* shapes, const int64_t* lsi,
-                                      const void* loc, const void* attn,
-                                      const void* grad_out, int N, int S, int M, int D,
-                                      int L, int Lq, int P, void* grad_value,
-                                      void* grad_loc, void* grad_attn,
-                                      gd_stream_t stream) {
+extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
+                                           const int64_t* shapes, const int64_t* lsi,
+                                           const void* loc, const void* attn,
+                                           const void* grad_out, int N, int S, int M, int D,
+                                           int L, int Lq, int P, void* grad_value,
+                                           void* grad_loc, void* grad_attn,
+                                           const int64_t* shapes_host, gd_stream_t stream) {
   gd_status st0 = check_common(dt, N, S, M, D, L, Lq, P);
   if (st0 != GD_OK) return st0;
   hipStream_t s = as_hip(stream);
@@ -153,20 +153,36 @@ extern "C" gd_status gd_msda_backward(gd_dtype dt, const void* value,
   // backward with LDS pre-aggregation.  Cross-attention (the decoder's 900
   // score-sorted queries) keeps the direct-atomic kernel.
   if ((dt == GD_F32 || dt == GD_BF16) && lane_ok && Lq == S && tiled_bwd_enabled()) {
-    const int tiles_per_n = (Lq + kTileQ - 1) / kTileQ;
+    // 2-D pixel tiles when the host knows the level grid (and it covers the
+    // S queries exactly); otherwise strips of kTileQ consecutive queries
+    int tiles_per_n = (Lq + kTileQ - 1) / kTileQ, tiles2d = 0;
+    if (shapes_host) {
+      int64_t cover = 0, nt = 0;
+      bool ok = true;
+      for (int l = 0; l < L; ++l) {
+        const int64_t h = shapes_host[2 * l], w = shapes_host[2 * l + 1];
+        ok = ok && h > 0 && w > 0;
+        cover += h * w;
+        nt += ((h + 3) / 4) * ((w + 7) / 8);
+      }
+      if (ok && cover == S && nt < (int64_t(1) << 30)) {
+        tiles_per_n = int(nt);
+        tiles2d = 1;
+      }
+    }
     const int64_t blocks = int64_t(N) * tiles_per_n * M;
     GD_REQUIRE(blocks < (int64_t(1) << 31), "msda_backward: grid too large");
     if (dt == GD_F32) {
       hipLaunchKernelGGL((msda_bwd_tiled<float, kTileQ, kTileRows>), dim3(int(blocks)), dim3(256), 0, s,
                      (const float*)value, shapes, lsi, (const float*)loc, (const float*)attn,
           (const float*)grad_out, (float*)grad_value, (float*)grad_loc, (float*)grad_attn,
-          S, Lq, M, tiles_per_n);
+          S, Lq, M, tiles_per_n, tiles2d);
       GD_LAUNCH_CHECK("msda_bwd_tiled<f32>");
     } else {
       hipLaunchKernelGGL((msda_bwd_tiled<uint16_t, kTileQ, kTileRows>), dim3(int(blocks)), dim3(256), 0, s,
                      (const uint16_t*)value, shapes, lsi, (const float*)loc, (const float*)attn,
           (const uint16_t*)grad_out, (float*)grad_value, (float*)grad_loc, (float*)grad_attn,
-          S, Lq, M, tiles_per_n);
+          S, Lq, M, tiles_per_n, tiles2d);
       GD_LAUNCH_CHECK("msda_bwd_tiled<bf16>");
     }
     return GD_OK;
@@ -211,4 +227,15 @@ extern "C" gd_status gd_msda_backward(gd_dtype dt, const void* value,
     GD_LAUNCH_CHECK("msda_bwd_generic<f64>");
   }
   return GD_OK;
+}
+
+extern "C" gd_status gd_msda_backward(gd_dtype dt, const void* value,
+                                      const int64_t* shapes, const int64_t* lsi,
+                                      const void* loc, const void* attn,
+                                      const void* grad_out, int N, int S, int M, int D,
+                                      int L, int Lq, int P, void* grad_value,
+                                      void* grad_loc, void* grad_attn,
+                                      gd_stream_t stream) {
+  return gd_msda_backward_geom(dt, value, shapes, lsi, loc, attn, grad_out, N, S, M, D, L, Lq, P,
+                               grad_value, grad_loc, grad_attn, nullptr, stream);
 }

@@ -38,6 +38,7 @@ _f = ctypes.c_float
 _SIGNATURES = {
     "gd_msda_forward": [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p],
     "gd_msda_backward": [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p],
+    "gd_msda_backward_geom": [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
 }
 
 

@@ -14,6 +14,8 @@ fp32), and launch errors raise instead of being printed.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -109,12 +111,20 @@ def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_lo
     return out
 
 
+def host_level_shapes(spatial_shapes):
+    """The host copy of the level shapes the model attaches to its cached
+    spatial_shapes tensor (``gd_host_shapes``), or None.  Never syncs."""
+    return getattr(spatial_shapes, "gd_host_shapes", None)
+
+
 def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
-                            grad_output, im2col_step: int = 64, grad_value_dtype=None):
+                            grad_output, im2col_step: int = 64, grad_value_dtype=None, host_shapes=None):
     """-> [grad_value, grad_sampling_loc, grad_attn_weight].
 
     grad_value is accumulated in fp32 (fp64 for fp64 value); it is returned in
-    ``grad_value_dtype`` (default: value.dtype, as the reference)."""
+    ``grad_value_dtype`` (default: value.dtype, as the reference).
+    ``host_shapes`` ([(H, W)] per level, host ints) lets the encoder-shape
+    backward tile by pixel blocks (gd_msda_backward_geom)."""
     (N, S, M, D, L, Lq, P), loc, attn = _check(value, spatial_shapes, level_start_index,
                                                sampling_loc, attn_weight, im2col_step,
                                                extra=(grad_output,))
@@ -127,11 +137,14 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     grad_value = torch.empty((N, S, M, D), dtype=acc, device=value.device)
     grad_loc = torch.empty((N, Lq, M, L, P, 2), dtype=acc, device=value.device)
     grad_attn = torch.empty((N, Lq, M, L, P), dtype=acc, device=value.device)
+    hs = None
+    if host_shapes is not None and len(host_shapes) == L:
+        hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
     t0 = timer.begin() if timer is not None else None
-    _lib.call("gd_msda_backward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
+    _lib.call("gd_msda_backward_geom", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
               level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), grad_output.data_ptr(),
               N, S, M, D, L, Lq, P, grad_value.data_ptr(), grad_loc.data_ptr(), grad_attn.data_ptr(),
-              _lib.stream_of(value))
+              hs, _lib.stream_of(value))
     if t0 is not None:
         timer.end("bwd", Lq, algorithmic_bytes("bwd", N, S, M, D, L, Lq, P, value.element_size()), t0)
     out_dtype = value.dtype if grad_value_dtype is None else grad_value_dtype

@@ -23,6 +23,7 @@ class MSDeformAttnFunction(Function):
     def forward(ctx, value, value_spatial_shapes, value_level_start_index, sampling_locations,
                 attention_weights, im2col_step):
         ctx.im2col_step = im2col_step
+        ctx.host_shapes = MSDA.host_level_shapes(value_spatial_shapes)
         output = MSDA.ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index,
                                              sampling_locations, attention_weights, im2col_step)
         ctx.save_for_backward(value, value_spatial_shapes, value_level_start_index,
@@ -37,7 +38,8 @@ class MSDeformAttnFunction(Function):
         # to value.dtype if they differ (one pass either way).
         grad_value, grad_loc, grad_attn = MSDA.ms_deform_attn_backward(
             value, shapes, lsi, loc, attn, grad_output.contiguous(), ctx.im2col_step,
-            grad_value_dtype=torch.float64 if value.dtype == torch.float64 else torch.float32)
+            grad_value_dtype=torch.float64 if value.dtype == torch.float64 else torch.float32,
+            host_shapes=ctx.host_shapes)
         return grad_value, None, None, grad_loc, grad_attn, None
 
 

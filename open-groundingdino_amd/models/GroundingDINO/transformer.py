@@ -141,6 +141,8 @@ class Transformer(nn.Module):
         key = tuple(shapes_list)
         spatial_shapes = device_const(("shapes",) + key,
                                       lambda: torch.as_tensor(shapes_list, dtype=torch.long), device)
+        # host copy for the MSDA backward's pixel-block tiling (no device sync)
+        spatial_shapes.gd_host_shapes = key
         level_start_index = device_const(("lsi",) + key, lambda: torch.as_tensor(starts, dtype=torch.long), device)
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
 

@@ -29,6 +29,7 @@ def lib():
         _LIB = ctypes.CDLL(os.path.join(EMU_DIR, "_build", "libgd_emu_asan.so" if asan else "libgd_emu.so"))
         _LIB.gd_msda_forward.argtypes = [_i, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p]
         _LIB.gd_msda_backward.argtypes = [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p, _p, _p]
+        _LIB.gd_msda_backward_geom.argtypes = [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p, _p, _p, _p]
         _LIB.gd_biattn_workspace_bytes.argtypes = [_i] * 4
         _LIB.gd_biattn_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_biattn_softmax_fwd.argtypes = [_i, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]
@@ -70,8 +71,9 @@ def msda_forward(value, shapes, lsi, loc, attn):
     return out
 
 
-def msda_backward(value, shapes, lsi, loc, attn, grad_out):
-    """-> grad_value (f32, or f64 for f64 value), grad_loc, grad_attn."""
+def msda_backward(value, shapes, lsi, loc, attn, grad_out, host_shapes=None):
+    """-> grad_value (f32, or f64 for f64 value), grad_loc, grad_attn.
+    host_shapes: [(H, W)] -> gd_msda_backward_geom (pixel-block tiles)."""
     N, S, M, D = value.shape
     _, Lq, _, L, P, _ = loc.shape
     acc = torch.float64 if value.dtype == torch.float64 else torch.float32
@@ -80,8 +82,14 @@ def msda_backward(value, shapes, lsi, loc, attn, grad_out):
     gv = torch.empty(N, S, M, D, dtype=acc)
     gl = torch.empty(N, Lq, M, L, P, 2, dtype=acc)
     ga = torch.empty(N, Lq, M, L, P, dtype=acc)
-    _check(lib().gd_msda_backward(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc), _ptr(attn),
-                                  _ptr(grad_out), N, S, M, D, L, Lq, P, _ptr(gv), _ptr(gl), _ptr(ga), None))
+    if host_shapes is None:
+        _check(lib().gd_msda_backward(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc), _ptr(attn),
+                                      _ptr(grad_out), N, S, M, D, L, Lq, P, _ptr(gv), _ptr(gl), _ptr(ga), None))
+    else:
+        hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
+        _check(lib().gd_msda_backward_geom(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc),
+                                           _ptr(attn), _ptr(grad_out), N, S, M, D, L, Lq, P, _ptr(gv), _ptr(gl),
+                                           _ptr(ga), hs, None))
     return gv, gl, ga
 
 

@@ -58,8 +58,8 @@ def _oracle_bwd(value, shapes, lsi, loc, attn, grad_out):
                                 grad_out.double().numpy())
 
 
-def _check_bwd(inputs, tol):
-    gv, gl, ga = E.msda_backward(*inputs)
+def _check_bwd(inputs, tol, host_shapes=None):
+    gv, gl, ga = E.msda_backward(*inputs, host_shapes=host_shapes)
     rgv, rgl, rga = _oracle_bwd(*inputs)
     assert E.rel_err(gv, rgv) < tol
     assert E.rel_err(gl, rgl) < tol
@@ -97,6 +97,30 @@ def test_emulated_tiled_backward_matches_oracle(levels, n, local, outliers):
     S = sum(h * w for h, w in levels)
     inputs = _levels_inputs(levels, n, S, seed=S + n, local=local, outlier_frac=outliers)
     _check_bwd(inputs, 1e-5)
+
+
+@pytest.mark.parametrize("levels,n,local,outliers", [
+    (SMALL, 1, False, 0.0),
+    (MEDIUM, 2, True, 0.0),     # partial 4 x 8 blocks at every level's right / bottom edge
+    (MEDIUM, 2, True, 0.1),
+    (WIDE, 1, True, 0.02),
+])
+def test_emulated_pixel_block_tiles_match_oracle(levels, n, local, outliers):
+    """gd_msda_backward_geom: 4 x 8 pixel-block tiles of each level (host
+    level shapes given) -- same sums as the oracle and the strip tiling."""
+    S = sum(h * w for h, w in levels)
+    inputs = _levels_inputs(levels, n, S, seed=S + 7 * n, local=local, outlier_frac=outliers)
+    blocks = _check_bwd(inputs, 1e-5, host_shapes=levels)
+    strips = E.msda_backward(*inputs)
+    torch.testing.assert_close(blocks[0], strips[0], rtol=1e-5, atol=1e-6)
+    assert torch.equal(blocks[1], strips[1]) and torch.equal(blocks[2], strips[2])
+
+
+def test_emulated_geom_falls_back_when_levels_do_not_tile_the_queries():
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 1, S, seed=21, local=True)
+    wrong = [(h, w + 1) for h, w in MEDIUM]  # covers more than S: strip tiling
+    _check_bwd(inputs, 1e-5, host_shapes=wrong)
 
 
 def test_emulated_tiled_backward_bf16():
@@ -164,6 +188,7 @@ S = sum(h * w for h, w in t.MEDIUM)
 t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=11, local=True, outlier_frac=0.1), 1e-5)
 t._check_bwd(t._levels_inputs(t.SMALL, 1, sum(h * w for h, w in t.SMALL), seed=12), 1e-5)
 t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 29, seed=13), 1e-5)
+t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=14, local=True, outlier_frac=0.1), 1e-5, host_shapes=t.MEDIUM)
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 2, 300, 40))
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 1, 130, 256))
 t.test_emulated_window_attention(7, 3, 8, 4, True, torch.float32, 1e-5)
@@ -196,6 +221,8 @@ S = sum(h * w for h, w in t.MEDIUM)
 t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=3, local=True, outlier_frac=0.1), 1e-5)
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)
 t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 37, seed=6), 1e-5)
+t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=8, local=True, outlier_frac=0.02), 1e-5,
+             host_shapes=t.WIDE)
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 2, 200, 100))
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
 t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)

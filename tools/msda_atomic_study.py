@@ -81,5 +81,62 @@ def main():
                   f"({distinct * 2 / 1e6:.2f} M per launch at bs=2 vs {total_valid * 2 / 1e6:.2f} M)")
 
 
+def kernel_policy(taps, tiles, shapes, starts, nrows=384):
+    """Global atomics of msda_bwd_tiled's policy (msda_tiled.inc): per tile
+    and head, each level's bounding box of corner rows is packed smallest
+    first into an nrows-row LDS accumulator; taps in a packed box cost one
+    flush atomic per distinct touched row, the others one atomic each."""
+    sizes = [h * w for h, w in shapes]
+    glob = 0
+    for qs in tiles:
+        blk = taps[qs]
+        for m in range(M):
+            v = blk[:, m].ravel()
+            v = v[v >= 0]
+            boxes = []
+            for li, (h, w) in enumerate(shapes):
+                vl = v[(v >= starts[li]) & (v < starts[li] + sizes[li])] - starts[li]
+                if len(vl) == 0:
+                    continue
+                y, x = vl // w, vl % w
+                boxes.append(((y.max() - y.min() + 1) * (x.max() - x.min() + 1), len(vl), len(np.unique(vl))))
+            used = 0
+            for area, n_taps, n_rows in sorted(boxes):
+                if used + area <= nrows:
+                    used += area
+                    glob += n_rows
+                else:
+                    glob += n_taps
+    return glob
+
+
+def policy_main():
+    shapes = LEVELS
+    sizes = [h * w for h, w in shapes]
+    starts = np.cumsum([0] + sizes[:-1])
+    S = sum(sizes)
+    refs = []
+    for h, w in shapes:
+        yy, xx = np.meshgrid((np.arange(h) + 0.5) / h, (np.arange(w) + 0.5) / w, indexing="ij")
+        refs.append(np.stack([xx.ravel(), yy.ravel()], -1))
+    ref = np.concatenate(refs)
+    taps = taps_for_queries(np.arange(S), ref, shapes, starts, init_offsets())
+    total = int((taps >= 0).sum())
+    strips = [np.arange(q0, min(q0 + 32, S)) for q0 in range(0, S, 32)]
+    blocks = []
+    for li, (h, w) in enumerate(shapes):
+        for y0 in range(0, h, 4):
+            for x0 in range(0, w, 8):
+                yy, xx = np.meshgrid(np.arange(y0, min(y0 + 4, h)), np.arange(x0, min(x0 + 8, w)), indexing="ij")
+                blocks.append(starts[li] + (yy * w + xx).ravel())
+    print("msda_bwd_tiled policy (384-row LDS boxes, global atomics per launch at bs=2):")
+    for name, tiles in (("32 consecutive queries (gd_msda_backward)", strips),
+                        ("4 x 8 pixel blocks (gd_msda_backward_geom)", blocks)):
+        g = kernel_policy(taps, tiles, shapes, starts)
+        print(f"  {name:44s} {g * 2 / 1e6:6.2f} M  ({total / g:.2f}x fewer than the direct kernel's "
+              f"{total * 2 / 1e6:.2f} M)")
+
+
 if __name__ == "__main__":
     main()
+    policy_main()
