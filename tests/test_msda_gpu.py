@@ -210,10 +210,11 @@ def _encoder_inputs(levels, n, seed, vdtype, spread_px=2.0, outlier_frac=0.0):
     return (value.to(vdtype), shapes, lsi, loc.float(), attn.float(), grad_out.to(vdtype))
 
 
-def _check_bwd_vs_oracle(inputs, tol):
+def _check_bwd_vs_oracle(inputs, tol, host_shapes=None):
     value, shapes, lsi, loc, attn, grad_out = inputs
     dev = [t.to(DEV) for t in inputs]
-    gv, gl, ga = _msda().ms_deform_attn_backward(*dev, 64, grad_value_dtype=torch.float32)
+    gv, gl, ga = _msda().ms_deform_attn_backward(*dev, 64, grad_value_dtype=torch.float32,
+                                                 host_shapes=host_shapes)
     torch.cuda.synchronize()
     v = value.double().numpy()
     ref_gv, ref_gl, ref_ga = oracle.msda_backward(v, shapes, lsi, loc.double(), attn.double(),
@@ -236,6 +237,20 @@ def test_encoder_tiled_backward_small(levels, n, outliers):
 @pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
 def test_encoder_tiled_backward_800x1333(vdtype, tol):
     _check_bwd_vs_oracle(_encoder_inputs(LEVELS_800, 2, seed=7, vdtype=vdtype, outlier_frac=0.01), tol)
+
+
+@pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+def test_encoder_pixel_block_backward_800x1333(vdtype, tol):
+    """gd_msda_backward_geom (host level shapes -> 4 x 8 pixel-block tiles),
+    the path the model's encoder takes."""
+    _check_bwd_vs_oracle(_encoder_inputs(LEVELS_800, 2, seed=8, vdtype=vdtype, outlier_frac=0.01), tol,
+                         host_shapes=LEVELS_800)
+
+
+@pytest.mark.parametrize("levels", [[(6, 9), (3, 5), (2, 3), (1, 2)], [(13, 21), (7, 11), (4, 6), (2, 3)]])
+def test_encoder_pixel_block_backward_small(levels):
+    _check_bwd_vs_oracle(_encoder_inputs(levels, 2, seed=3, vdtype=torch.float32, outlier_frac=0.05), 1e-3,
+                         host_shapes=levels)
 
 
 def test_encoder_tiled_matches_direct_atomic_kernel(monkeypatch):
