@@ -46,6 +46,10 @@
  *                        text enhancer's and the decoder's
  *                        nn.MultiheadAttention (transformer_vanilla.py:83,
  *                        transformer.py:839,844)
+ *   gd_msda_prologue_forward / _backward
+ *                     <- the MSDA module's softmax over L*P and sampling-
+ *                        location math (reference_points + offsets /
+ *                        normalizer) models/GroundingDINO/ms_deform_attn.py:274-363
  *   gd_contrastive_forward
  *                     <- ContrastiveEmbed.forward (x . text^T, -inf on padded
  *                        tokens, -inf right padding to max_text_len)
@@ -136,6 +140,28 @@ gd_status gd_msda_backward_geom(gd_dtype value_dtype, const void* value,
                                 void* grad_value, void* grad_sampling_loc,
                                 void* grad_attn_weight, const int64_t* spatial_shapes_host,
                                 gd_stream_t stream);
+
+/*
+ * MSDA prologue (ms_deform_attn.py:274-363): offsets [N, Lq, M*L*P*2] and
+ * attention logits [N, Lq, M*L*P] (F32 or BF16, contiguous rows with the
+ * given row strides in elements), reference_points [N, Lq, L, ref_dim] F32
+ * (ref_dim 2: + offsets / (W_l, H_l); 4: + offsets / P * wh * 0.5),
+ * spatial_shapes [L][2] int64 on the device; L*P == 16.
+ * -> sampling_loc [N, Lq, M, L, P, 2] F32, attn_weight [N, Lq, M, L, P] F32
+ *    (softmax over each unit's L*P logits).
+ * Backward -> grad_offsets / grad_logits, contiguous, in the input dtype;
+ * the reference points get no gradient.
+ */
+gd_status gd_msda_prologue_forward(gd_dtype dtype, const void* offsets, int64_t offsets_row_stride,
+                                   const void* logits, int64_t logits_row_stride,
+                                   const float* reference_points, int ref_dim,
+                                   const int64_t* spatial_shapes, int N, int Lq, int M, int L, int P,
+                                   float* sampling_loc, float* attn_weight, gd_stream_t stream);
+gd_status gd_msda_prologue_backward(gd_dtype dtype, const float* grad_loc, const float* grad_attn,
+                                    const float* attn_weight, const float* reference_points,
+                                    int ref_dim, const int64_t* spatial_shapes, int N, int Lq, int M,
+                                    int L, int P, void* grad_offsets, void* grad_logits,
+                                    gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* BiAttention bidirectional softmax (fuse_modules.py:174-217)               */

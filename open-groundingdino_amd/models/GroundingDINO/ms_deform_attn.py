@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 from torch.nn.init import constant_, xavier_uniform_
 
-from gdino_amd import castcache
+from gdino_amd import castcache, msda_prologue
 
 from .ops.functions.ms_deform_attn_func import MSDeformAttnFunction
 
@@ -95,10 +95,16 @@ def msda_attend(mod, query, value, reference_points, spatial_shapes, level_start
         value = value.masked_fill(key_padding_mask[..., None], 0.0)
     value = value.view(bs, num_value, num_heads, -1)
     offsets, attn = castcache.linear_shared_input(query, (mod.sampling_offsets, mod.attention_weights))
-    offsets = offsets.reshape(bs, num_query, num_heads, num_levels, num_points, 2)
-    attn = attn.reshape(bs, num_query, num_heads, num_levels * num_points)
-    attn = attn.to(_loc_dtype(attn)).softmax(-1).view(bs, num_query, num_heads, num_levels, num_points)
-    loc = sampling_locations_from(reference_points, offsets, spatial_shapes, num_points)
+    if msda_prologue.supported(offsets, attn, reference_points, num_levels, num_points):
+        # softmax + sampling-location math as one kernel each way
+        # (gdino_amd/msda_prologue.py)
+        loc, attn = msda_prologue.MSDAPrologue.apply(offsets, attn, reference_points, spatial_shapes, num_heads,
+                                                     num_levels, num_points)
+    else:
+        offsets = offsets.reshape(bs, num_query, num_heads, num_levels, num_points, 2)
+        attn = attn.reshape(bs, num_query, num_heads, num_levels * num_points)
+        attn = attn.to(_loc_dtype(attn)).softmax(-1).view(bs, num_query, num_heads, num_levels, num_points)
+        loc = sampling_locations_from(reference_points, offsets, spatial_shapes, num_points)
     if value.dtype == torch.float16:  # kernels run fp32 / bf16 / fp64 value
         value = value.float()
     out = MSDeformAttnFunction.apply(value.contiguous(), spatial_shapes, level_start_index,

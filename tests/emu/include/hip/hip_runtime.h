@@ -61,6 +61,9 @@ inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c,
 inline uint2 make_uint2(unsigned a, unsigned b) { return {a, b}; }
 inline uint4 make_uint4(unsigned a, unsigned b, unsigned c, unsigned d) { return {a, b, c, d}; }
 inline float __logf(float x) { return logf(x); }
+inline float __fadd_rn(float a, float b) { return a + b; }
+inline float __fmul_rn(float a, float b) { return a * b; }
+inline float __fdiv_rn(float a, float b) { return a / b; }
 
 typedef int hipError_t;
 constexpr hipError_t hipSuccess = 0;

@@ -41,6 +41,9 @@ def lib():
         _LIB.gd_attn_forward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u, _p, _p, _p, _p]
         _LIB.gd_attn_backward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u] + [_p] * 13
         _LIB.gd_contrastive_forward.argtypes = [_i] + [_p] * 5 + [_i] * 5 + [_p, _p, _p]
+        _i64 = ctypes.c_int64
+        _LIB.gd_msda_prologue_forward.argtypes = [_i, _p, _i64, _p, _i64, _p, _i, _p] + [_i] * 5 + [_p, _p, _p]
+        _LIB.gd_msda_prologue_backward.argtypes = [_i, _p, _p, _p, _p, _i, _p] + [_i] * 5 + [_p, _p, _p]
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -211,6 +214,32 @@ def contrastive_forward(x, text, mask, tout, want_logits=True, want_rowmax=True)
                                         (ctypes.c_int64 * 2)(*text.stride()[:2]), _ptr(keep), B, Q, T, C, tout,
                                         _ptr(logits), _ptr(rowmax), None))
     return logits, rowmax
+
+
+def msda_prologue_forward(offsets, logits, ref, shapes, M, L, P):
+    """offsets [N, Lq, M*L*P*2], logits [N, Lq, M*L*P] (row-strided views
+    allowed), ref [N, Lq, L, 2|4] f32 -> loc [N, Lq, M, L, P, 2], attn"""
+    N, Lq, _ = offsets.shape
+    ref = ref.float().contiguous()
+    shapes = shapes.to(torch.int64).contiguous()
+    loc = torch.full((N, Lq, M, L, P, 2), float("nan"))
+    attn = torch.full((N, Lq, M, L, P), float("nan"))
+    _check(lib().gd_msda_prologue_forward(_code(offsets), _ptr(offsets), offsets.stride(1), _ptr(logits),
+                                          logits.stride(1), _ptr(ref), ref.shape[-1], _ptr(shapes), N, Lq, M, L, P,
+                                          _ptr(loc), _ptr(attn), None))
+    return loc, attn
+
+
+def msda_prologue_backward(grad_loc, grad_attn, attn, ref, shapes, dtype):
+    N, Lq, M, L, P = attn.shape
+    ref = ref.float().contiguous()
+    shapes = shapes.to(torch.int64).contiguous()
+    g_off = torch.full((N, Lq, M * L * P * 2), float("nan")).to(dtype)
+    g_log = torch.full((N, Lq, M * L * P), float("nan")).to(dtype)
+    _check(lib().gd_msda_prologue_backward(_code(g_off), _ptr(grad_loc.contiguous()), _ptr(grad_attn.contiguous()),
+                                           _ptr(attn), _ptr(ref), ref.shape[-1], _ptr(shapes), N, Lq, M, L, P,
+                                           _ptr(g_off), _ptr(g_log), None))
+    return g_off, g_log
 
 
 def attn_dropout_keep(B, H, Lq, Lk, p, seed):

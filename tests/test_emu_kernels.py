@@ -416,3 +416,37 @@ def test_emulated_contrastive(B, Q, T, C, tout, dtype, tol):
     assert E.rel_err(rowmax, ref.max(-1)[0]) < tol
     _, only_max = E.contrastive_forward(x, text, mask, T, want_logits=False)
     assert torch.equal(only_max, rowmax)
+
+
+# ------------------------------------------------------ MSDA prologue
+@pytest.mark.parametrize("ref_dim", [2, 4])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_emulated_msda_prologue(ref_dim, dtype):
+    """softmax + sampling-location math (ms_deform_attn.py:274-363) against
+    the product's torch composition (itself pinned by the Transformer
+    goldens): loc bit-identical, attn and both gradients to fp32 rounding."""
+    from models.GroundingDINO.ms_deform_attn import sampling_locations_from
+    g = torch.Generator().manual_seed(ref_dim)
+    N, Lq, M, L, P = 2, 37, 8, 4, 4
+    shapes = torch.as_tensor([(13, 21), (7, 11), (4, 6), (2, 3)])
+    proj = (torch.randn(N, Lq, M * L * P * 3, generator=g) * 3).to(dtype)  # the fused Linear output
+    off, logit = proj[..., :M * L * P * 2], proj[..., M * L * P * 2:]   # row-strided views, read in place
+    ref = torch.rand(N, Lq, L, ref_dim, generator=g)
+    loc, attn = E.msda_prologue_forward(off, logit, ref, shapes, M, L, P)
+    offd = off.float().requires_grad_(True)
+    logd = logit.float().requires_grad_(True)
+    rl = sampling_locations_from(ref, offd.reshape(N, Lq, M, L, P, 2), shapes, P)
+    ra = logd.reshape(N, Lq, M, L * P).softmax(-1).view(N, Lq, M, L, P)
+    assert torch.equal(loc, rl.detach())
+    torch.testing.assert_close(attn, ra.detach(), rtol=1e-6, atol=1e-7)
+    gl = torch.randn(loc.shape, generator=g)
+    ga = torch.randn(attn.shape, generator=g)
+    (rl * gl).sum().backward()
+    (ra * ga).sum().backward()
+    g_off, g_log = E.msda_prologue_backward(gl, ga, attn, ref, shapes, dtype)
+    if dtype == torch.float32:
+        assert torch.equal(g_off, offd.grad)
+        torch.testing.assert_close(g_log, logd.grad, rtol=1e-5, atol=1e-6)
+    else:  # the reference returns these grads through the bf16 cast as well
+        assert torch.equal(g_off, offd.grad.to(dtype))
+        torch.testing.assert_close(g_log.float(), logd.grad.to(dtype).float(), rtol=1e-2, atol=1e-3)

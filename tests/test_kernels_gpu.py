@@ -239,3 +239,33 @@ def test_contrastive_logits_and_rowmax(dtype, tol, b, q, t):
     assert _rel(tg.grad.cpu(), td.grad) < tol * 3
     rm = contrastive_rowmax_hip(x.to(DEV), text.to(DEV), mask.to(DEV)).cpu()
     assert _rel(rm, ref.detach().max(-1)[0]) < tol
+
+
+# ------------------------------------------------------ MSDA prologue (HIP)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ref_dim,lq", [(2, 22223), (4, 900)])  # encoder / decoder shapes at 800x1333 bs=2
+def test_msda_prologue_matches_composition(dtype, ref_dim, lq):
+    from gdino_amd.msda_prologue import MSDAPrologue, supported
+    from models.GroundingDINO.ms_deform_attn import sampling_locations_from
+    g = torch.Generator().manual_seed(lq)
+    N, M, L, P = 2, 8, 4, 4
+    shapes = torch.as_tensor([(100, 167), (50, 84), (25, 42), (13, 21)]).to(DEV)
+    proj = (torch.randn(N, lq, 384, generator=g) * 3).to(dtype).to(DEV)
+    off = proj[..., :256].requires_grad_(False)
+    logit = proj[..., 256:]
+    ref = torch.rand(N, lq, L, ref_dim, generator=g).to(DEV)
+    assert supported(off, logit, ref, L, P)
+    o1, l1 = off.detach().clone().requires_grad_(True), logit.detach().clone().requires_grad_(True)
+    loc, attn = MSDAPrologue.apply(o1, l1, ref, shapes, M, L, P)
+    o2, l2 = off.detach().clone().requires_grad_(True), logit.detach().clone().requires_grad_(True)
+    rl = sampling_locations_from(ref, o2.reshape(N, lq, M, L, P, 2), shapes, P)
+    ra = l2.reshape(N, lq, M, L * P).float().softmax(-1).view(N, lq, M, L, P)
+    torch.testing.assert_close(loc, rl, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(attn, ra, rtol=1e-5, atol=1e-6)
+    gl = torch.randn(loc.shape, generator=g).to(DEV)
+    ga = torch.randn(attn.shape, generator=g).to(DEV)
+    ((loc * gl).sum() + (attn * ga).sum()).backward()
+    ((rl * gl).sum() + (ra * ga).sum()).backward()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(o1.grad.float().cpu(), o2.grad.float().cpu()) < tol
+    assert _rel(l1.grad.float().cpu(), l2.grad.float().cpu()) < tol

@@ -161,6 +161,26 @@ def main():
         finally:
             counter.paused -= 1
 
+    # the MSDA prologue kernel (GPU-only, gdino_amd/msda_prologue.py): one
+    # launch each way, computed here by the torch composition
+    from gdino_amd import msda_prologue as pro_mod
+
+    def pro_fn(off, logit, ref, shapes, m, l, p):
+        n, lq, _ = off.shape
+        loc = msda_mod.sampling_locations_from(ref, off.float().reshape(n, lq, m, l, p, 2), shapes, p)
+        attn = logit.float().reshape(n, lq, m, l * p).softmax(-1).view(n, lq, m, l, p)
+        return loc, attn
+
+    pro_op = counted(pro_fn, "gd.msda_prologue")
+
+    class CountedPrologue:
+        @staticmethod
+        def apply(*x):
+            return pro_op(*x)
+
+    prev_pro = (pro_mod.supported, pro_mod.MSDAPrologue)
+    pro_mod.supported = lambda off, logit, ref, l, p: l * p == 16 and not ref.requires_grad
+    pro_mod.MSDAPrologue = CountedPrologue
     prev = msda_mod.MSDeformAttnFunction
     msda_mod.MSDeformAttnFunction = CountedMSDA
     amp = None if a.no_autocast else torch.bfloat16
@@ -195,6 +215,7 @@ def main():
                 step(counter)
     finally:
         msda_mod.MSDeformAttnFunction = prev
+        pro_mod.supported, pro_mod.MSDAPrologue = prev_pro
     total = sum(counter.counts.values())
     casts = sum(v for k, v in counter.counts.items() if k.startswith("aten._to_copy"))
     print(f"dispatches/step={total} (+~25 fused AdamW on GPU)  casts={casts}  by phase: {dict(counter.by_phase)}")
