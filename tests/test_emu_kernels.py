@@ -230,6 +230,9 @@ t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
 t.test_emulated_attention(2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh")
 t.test_emulated_attention(1, 1, 33, 300, 32, "add", torch.float32, 1e-5, "blh")
 t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
+t.test_emulated_msda_prologue(2, torch.bfloat16)
+t.test_emulated_msda_prologue(4, torch.float32)
+t.test_emulated_attention_dropout(torch.float32, 1e-5)
 print("asan-clean")
 """
 
