@@ -140,4 +140,5 @@ def linear_shared_input(x: torch.Tensor, layers):
         return [m(x) for m in layers]
     w = _cached_cat([m.weight for m in layers], dt)
     b = _cached_cat([m.bias for m in layers], dt)
-    return list(F.linear(x, w, b).split([m.out_features for m in layers], dim=-1))
+    from .misc import split_last
+    return list(split_last(F.linear(x, w, b), [m.out_features for m in layers]))

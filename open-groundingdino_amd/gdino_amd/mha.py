@@ -17,6 +17,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from . import castcache
+from .misc import split_last
 
 
 def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor], b: int, h: int,
@@ -123,7 +124,7 @@ class MultiheadAttention(nn.Module):
         e = self.embed_dim
         w, bias = self.in_proj_weight, self.in_proj_bias
         if query is key and key is value:
-            return castcache.linear(query, w, bias).chunk(3, dim=-1)
+            return split_last(castcache.linear(query, w, bias), (e, e, e))
         dt = castcache.autocast_dtype(query)
         if dt is not None:
             w = castcache.cached_cast(w, dt)
@@ -133,19 +134,19 @@ class MultiheadAttention(nn.Module):
                 xa, xb = (query, value) if query is key else (query, key)
                 ya, yb = _PackedInProj.apply(w, bias, xa.to(dt), xb.to(dt), split)
                 if query is key:
-                    q, k = ya.chunk(2, dim=-1)
+                    q, k = split_last(ya, (e, e))
                     return q, k, yb
-                k, v = yb.chunk(2, dim=-1)
+                k, v = split_last(yb, (e, e))
                 return ya, k, v
 
         def lin(x, r0, r1):
             return F.linear(x, w[r0:r1], None if bias is None else bias[r0:r1])
 
         if query is key:
-            q, k = lin(query, 0, 2 * e).chunk(2, dim=-1)
+            q, k = split_last(lin(query, 0, 2 * e), (e, e))
             return q, k, lin(value, 2 * e, 3 * e)
         if key is value:
-            k, v = lin(key, e, 3 * e).chunk(2, dim=-1)
+            k, v = split_last(lin(key, e, 3 * e), (e, e))
             return lin(query, 0, e), k, v
         return lin(query, 0, e), lin(key, e, 2 * e), lin(value, 2 * e, 3 * e)
 

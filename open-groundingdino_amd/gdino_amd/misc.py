@@ -57,6 +57,33 @@ class NestedTensor:
         return f"NestedTensor(tensors={tuple(self.tensors.shape)}, mask={None if self.mask is None else tuple(self.mask.shape)})"
 
 
+class _SplitLast(torch.autograd.Function):
+    """x.split(sizes, -1) whose backward is ONE cat of the pieces' gradients
+    (autograd's split backward builds a zero-filled full-size gradient per
+    piece, copies it in and sums them: 3 kernels per piece)."""
+
+    @staticmethod
+    def forward(ctx, x, sizes):
+        ctx.sizes = sizes
+        ctx.meta = (x.shape[:-1], x.dtype, x.device)
+        return tuple(x.split(sizes, -1))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        lead, dt, dev = ctx.meta
+        gs = [g if g is not None else torch.zeros(*lead, n, dtype=dt, device=dev) for g, n in zip(grads, ctx.sizes)]
+        return torch.cat(gs, -1), None
+
+
+def split_last(x: Tensor, sizes) -> tuple:
+    """x.split(sizes, dim=-1) with a single-cat backward (same values and
+    gradients)."""
+    sizes = [int(n) for n in sizes]
+    if not (torch.is_grad_enabled() and x.requires_grad):
+        return tuple(x.split(sizes, -1))
+    return _SplitLast.apply(x, sizes)
+
+
 def nested_tensor_from_tensor_list(tensor_list) -> NestedTensor:
     """Zero-pad [C,H,W] images to the batch max size; mask marks the padding
     (groundingdino/util/misc.py:483-506)."""

@@ -422,8 +422,12 @@ class DeformableTransformerDecoderLayer(nn.Module):
             tgt2 = self.self_attn(q, k, tgt, attn_mask=self_attn_mask)[0]
             tgt = self.norm2(tgt + self.dropout2(tgt2))
         if self.use_text_cross_attention:
-            tgt2 = self.ca_text(self.with_pos_embed(tgt, tgt_query_pos), memory_text.transpose(0, 1),
-                                memory_text.transpose(0, 1), key_padding_mask=text_attention_mask)[0]
+            # key and value are the same tensor (reference :900-905 passes
+            # two identical transposes): one object lets the MHA project them
+            # with one GEMM
+            text_kv = memory_text.transpose(0, 1)
+            tgt2 = self.ca_text(self.with_pos_embed(tgt, tgt_query_pos), text_kv, text_kv,
+                                key_padding_mask=text_attention_mask)[0]
             tgt = self.catext_norm(tgt + self.catext_dropout(tgt2))
         tgt2 = self.cross_attn(query=self.with_pos_embed(tgt, tgt_query_pos).transpose(0, 1),
                                reference_points=tgt_reference_points.transpose(0, 1).contiguous(),
