@@ -50,6 +50,11 @@
  *                     <- the MSDA module's softmax over L*P and sampling-
  *                        location math (reference_points + offsets /
  *                        normalizer) models/GroundingDINO/ms_deform_attn.py:274-363
+ *   gd_wgrad / gd_wgrad_splits / gd_wgrad_workspace_bytes
+ *                     <- the weight / bias gradient of the token-heavy
+ *                        nn.Linear layers (autograd's dW = dY^T X GEMM), as a
+ *                        split-K fp32 reduction (no reference counterpart:
+ *                        torch autograd in the reference)
  *   gd_contrastive_forward
  *                     <- ContrastiveEmbed.forward (x . text^T, -inf on padded
  *                        tokens, -inf right padding to max_text_len)
@@ -260,6 +265,23 @@ gd_status gd_contrastive_forward(gd_dtype dtype, const void* x, const int64_t* x
                                  const void* text, const int64_t* text_strides,
                                  const uint8_t* text_mask, int B, int Q, int T, int C, int Tout,
                                  float* logits, float* rowmax, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Split-K weight gradient of token-heavy Linear layers                      */
+/* ------------------------------------------------------------------------ */
+/*
+ * grad_y [T, O] and x [T, I] (F32 or BF16) row-major with row strides ldy /
+ * ldx (elements, 16-byte aligned rows); O, I multiples of 64.
+ * grad_w [O, I] F32 = grad_y^T x;  grad_b [O] F32 = column sums of grad_y
+ * (or NULL).  Both are overwritten.  splits: token splits (gd_wgrad_splits
+ * gives the default); workspace: gd_wgrad_workspace_bytes(O, I, splits)
+ * bytes of device memory.  Deterministic (fixed-order reduction).
+ */
+int gd_wgrad_splits(int T, int O, int I);
+size_t gd_wgrad_workspace_bytes(int O, int I, int splits);
+gd_status gd_wgrad(gd_dtype dtype, const void* grad_y, int64_t ldy, const void* x, int64_t ldx, int T,
+                   int O, int I, int splits, void* workspace, float* grad_w, float* grad_b,
+                   gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

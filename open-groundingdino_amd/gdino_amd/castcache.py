@@ -82,13 +82,28 @@ def clear() -> None:
     _cache.clear()
 
 
+def _token_linear_ok(x, params, out_features, dt) -> bool:
+    """Route to gdino_amd.wgrad.token_linear (split-K weight gradient): the
+    GPU, bf16 autocast, trainable fp32 parameters, a qualifying shape."""
+    if dt != torch.bfloat16 or not torch.is_grad_enabled() or _capturing(params[0]):
+        return False
+    if any(p.dtype != torch.float32 or not p.requires_grad for p in params):
+        return False
+    from . import wgrad
+    return wgrad.eligible(x, out_features)
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     """F.linear with cached weight / bias casts under autocast."""
     dt = autocast_dtype(x) if ENABLED else None
     if dt is not None and weight.is_floating_point():
-        weight = cached_cast(weight, dt)
-        if bias is not None:
-            bias = cached_cast(bias, dt)
+        wc = cached_cast(weight, dt)
+        bc = None if bias is None else cached_cast(bias, dt)
+        params = [weight] + ([bias] if bias is not None else [])
+        if _token_linear_ok(x, params, weight.shape[0], dt):
+            from . import wgrad
+            return wgrad.token_linear(x, wc, bc, [weight], [] if bias is None else [bias])
+        return F.linear(x, wc, bc)
     return F.linear(x, weight, bias)
 
 
@@ -141,4 +156,10 @@ def linear_shared_input(x: torch.Tensor, layers):
     w = _cached_cat([m.weight for m in layers], dt)
     b = _cached_cat([m.bias for m in layers], dt)
     from .misc import split_last
-    return list(split_last(F.linear(x, w, b), [m.out_features for m in layers]))
+    params = [m.weight for m in layers] + [m.bias for m in layers]
+    if _token_linear_ok(x, params, w.shape[0], dt):
+        from . import wgrad
+        y = wgrad.token_linear(x, w, b, [m.weight for m in layers], [m.bias for m in layers])
+    else:
+        y = F.linear(x, w, b)
+    return list(split_last(y, [m.out_features for m in layers]))

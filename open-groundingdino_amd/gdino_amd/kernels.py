@@ -151,3 +151,4 @@ from . import wattn  # noqa: E402,F401
 from . import attn  # noqa: E402,F401
 from . import contrastive  # noqa: E402,F401
 from . import msda_prologue  # noqa: E402,F401
+from . import wgrad  # noqa: E402,F401

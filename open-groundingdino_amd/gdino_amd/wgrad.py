@@ -1,0 +1,102 @@
+"""Token-heavy Linear layers with a split-K weight-gradient kernel
+(csrc/wgrad.hip) on MI355X.
+
+For a Linear over T tokens with a small O x I weight (the encoder's
+value / output / sampling projections: T = 44 446 at 800x1333 bs=2, 256 x 256
+to 384 x 256; Swin stage 2: T = 33 400, 192-wide), the library GEMM for
+dW = dY^T X tiles only the O x I output (16-24 tiles of 64 x 64 on 256 CUs).
+``token_linear`` keeps the forward and dX GEMMs on hipBLASLt and computes dW
+and db with the split-K kernel, in fp32, straight into the fp32 master
+parameters' gradients (no bf16 weight-gradient rounding, no bf16 -> fp32
+cast kernel per weight).  Numerically it is the same product with fp32
+accumulation; tested against the fp64 reference in tests/test_kernels_gpu.py.
+
+Used by castcache.linear / linear_shared_input under autocast on the GPU
+when the shape qualifies (``eligible``); everything else is unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+_p, _i, _i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+_lib.register("gd_wgrad", [_i, _p, _i64, _p, _i64, _i, _i, _i, _i, _p, _p, _p, _p])
+_lib.register("gd_wgrad_splits", [_i, _i, _i])  # returns int (the registered restype)
+
+MIN_TOKENS = 4096
+MAX_TILES = 32  # O/64 * I/64: beyond this the library GEMM has enough output tiles
+ENABLED = True
+
+
+def eligible(x: torch.Tensor, out_features: int) -> bool:
+    in_features = x.shape[-1]
+    if not (ENABLED and x.is_cuda and out_features % 64 == 0 and in_features % 64 == 0):
+        return False
+    tokens = x.numel() // max(in_features, 1)
+    return tokens >= MIN_TOKENS and (out_features // 64) * (in_features // 64) <= MAX_TILES
+
+
+def _splits(t, o, i):
+    return int(_lib.lib().gd_wgrad_splits(t, o, i))
+
+
+def _workspace(o, i, s, device):
+    fn = _lib.lib().gd_wgrad_workspace_bytes
+    fn.restype, fn.argtypes = ctypes.c_size_t, [_i, _i, _i]
+    return torch.empty((int(fn(o, i, s)) + 3) // 4, dtype=torch.float32, device=device)
+
+
+def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, want_bias: bool):
+    """dy2 [T, O], x2 [T, I] (same dtype, contiguous rows) -> dW [O, I] fp32,
+    db [O] fp32 or None."""
+    t, o = dy2.shape
+    i = x2.shape[1]
+    s = _splits(t, o, i)
+    ws = _workspace(o, i, s, dy2.device)
+    dw = torch.empty(o, i, dtype=torch.float32, device=dy2.device)
+    db = torch.empty(o, dtype=torch.float32, device=dy2.device) if want_bias else None
+    _lib.call("gd_wgrad", _lib.dtype_code(dy2), dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), t, o, i,
+              s, ws.data_ptr(), dw.data_ptr(), _lib.ptr(db), _lib.stream_of(dy2))
+    return dw, db
+
+
+class TokenLinear(torch.autograd.Function):
+    """y = x . wc^T + bc with wc / bc the low-precision copies of the fp32
+    parameters ``params`` (one or several row blocks of the weight, then the
+    matching bias blocks); gradients go to ``params`` in fp32."""
+
+    @staticmethod
+    def forward(ctx, x, wc, bc, nw, *params):
+        xc = x if x.dtype == wc.dtype else x.to(wc.dtype)
+        y = F.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.x_dtype = x.dtype
+        ctx.rows = [p.shape[0] for p in params[:nw]]
+        ctx.nw = nw
+        ctx.has_bias = len(params) > nw
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        dy = dy.to(wc.dtype)
+        dx = torch.matmul(dy, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+        i = xc.shape[-1]
+        dw, db = weight_grad(dy.reshape(-1, dy.shape[-1]).contiguous(), xc.reshape(-1, i).contiguous(),
+                             ctx.has_bias)
+        grads = list(dw.split(ctx.rows, 0))
+        if ctx.has_bias:
+            grads += list(db.split(ctx.rows, 0))
+        return (dx, None, None, None, *grads)
+
+
+def token_linear(x, wc, bc, weights, biases):
+    """F.linear(x, wc, bc) whose weight / bias gradients reach the fp32
+    ``weights`` / ``biases`` (row blocks of wc / bc) through the split-K
+    kernel."""
+    params = list(weights) + (list(biases) if bc is not None else [])
+    return TokenLinear.apply(x, wc.detach(), None if bc is None else bc.detach(), len(weights), *params)

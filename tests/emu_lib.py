@@ -44,6 +44,10 @@ def lib():
         _i64 = ctypes.c_int64
         _LIB.gd_msda_prologue_forward.argtypes = [_i, _p, _i64, _p, _i64, _p, _i, _p] + [_i] * 5 + [_p, _p, _p]
         _LIB.gd_msda_prologue_backward.argtypes = [_i, _p, _p, _p, _p, _i, _p] + [_i] * 5 + [_p, _p, _p]
+        _LIB.gd_wgrad.argtypes = [_i, _p, _i64, _p, _i64, _i, _i, _i, _i, _p, _p, _p, _p]
+        _LIB.gd_wgrad_splits.argtypes = [_i, _i, _i]
+        _LIB.gd_wgrad_workspace_bytes.argtypes = [_i, _i, _i]
+        _LIB.gd_wgrad_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -240,6 +244,19 @@ def msda_prologue_backward(grad_loc, grad_attn, attn, ref, shapes, dtype):
                                            _ptr(attn), _ptr(ref), ref.shape[-1], _ptr(shapes), N, Lq, M, L, P,
                                            _ptr(g_off), _ptr(g_log), None))
     return g_off, g_log
+
+
+def wgrad(dy, x, bias=True, splits=None):
+    """dy [T, O], x [T, I] (f32/bf16, row-major) -> dW [O, I] f32, db [O] f32"""
+    T, O = dy.shape
+    I = x.shape[1]
+    s = int(lib().gd_wgrad_splits(T, O, I)) if splits is None else splits
+    ws = torch.empty((int(lib().gd_wgrad_workspace_bytes(O, I, s)) + 3) // 4, dtype=torch.float32)
+    dw = torch.full((O, I), float("nan"))
+    db = torch.full((O,), float("nan")) if bias else None
+    _check(lib().gd_wgrad(_code(dy), _ptr(dy), dy.stride(0), _ptr(x), x.stride(0), T, O, I, s, _ptr(ws), _ptr(dw),
+                          _ptr(db), None))
+    return dw, db
 
 
 def attn_dropout_keep(B, H, Lq, Lk, p, seed):

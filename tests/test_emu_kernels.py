@@ -453,3 +453,23 @@ def test_emulated_msda_prologue(ref_dim, dtype):
     else:  # the reference returns these grads through the bf16 cast as well
         assert torch.equal(g_off, offd.grad.to(dtype))
         torch.testing.assert_close(g_log.float(), logd.grad.to(dtype).float(), rtol=1e-2, atol=1e-3)
+
+
+# ------------------------------------------- split-K weight gradient
+@pytest.mark.parametrize("T,O,I,splits,dtype,tol", [
+    (1000, 128, 64, None, torch.float32, 1e-6),   # token tail inside the last split
+    (777, 64, 192, 3, torch.float32, 1e-6),       # splits not dividing T, 3 column tiles
+    (300, 192, 128, 1, torch.bfloat16, 1e-6),     # bf16-exact inputs, fp32 accumulation
+    (64, 64, 64, 5, torch.float32, 1e-6),         # more splits than token chunks: empty splits
+])
+def test_emulated_wgrad(T, O, I, splits, dtype, tol):
+    g = torch.Generator().manual_seed(T + O)
+    dy = torch.randn(T, O, generator=g).to(dtype)
+    x = torch.randn(T, I, generator=g).to(dtype)
+    dw, db = E.wgrad(dy, x, splits=splits)
+    ref_w = dy.double().t() @ x.double()
+    ref_b = dy.double().sum(0)
+    assert E.rel_err(dw, ref_w) < tol * 10
+    assert E.rel_err(db, ref_b) < tol * 10
+    dw2, none = E.wgrad(dy, x, bias=False, splits=splits)
+    assert none is None and torch.equal(dw, dw2)

@@ -269,3 +269,50 @@ def test_msda_prologue_matches_composition(dtype, ref_dim, lq):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert _rel(o1.grad.float().cpu(), o2.grad.float().cpu()) < tol
     assert _rel(l1.grad.float().cpu(), l2.grad.float().cpu()) < tol
+
+
+# ----------------------------------------- split-K weight gradient (HIP)
+@pytest.mark.parametrize("T,O,I", [(44446, 256, 256), (44446, 384, 256), (33400, 192, 192), (5000, 128, 64)])
+def test_wgrad_kernel(T, O, I):
+    """encoder value / output / sampling projections at 800x1333 bs=2, Swin
+    stage-2 width; bf16 operands, fp32 results vs the fp64 product."""
+    from gdino_amd.wgrad import weight_grad
+    g = torch.Generator().manual_seed(T + O)
+    dy = torch.randn(T, O, generator=g).to(torch.bfloat16)
+    x = torch.randn(T, I, generator=g).to(torch.bfloat16)
+    dw, db = weight_grad(dy.to(DEV), x.to(DEV), True)
+    torch.cuda.synchronize()
+    assert _rel(dw.cpu(), dy.double().t() @ x.double()) < 1e-5
+    assert _rel(db.cpu(), dy.double().sum(0)) < 1e-5
+
+
+def test_token_linear_matches_autocast_linear():
+    """castcache.linear routes an eligible Linear through TokenLinear: same
+    output, and weight / bias / input gradients within bf16 noise of the
+    library path (wgrad.ENABLED = False), both against fp64."""
+    from gdino_amd import castcache, wgrad
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(256, 256).to(DEV)
+    x = torch.randn(2, 22223, 256, device=DEV)
+    gy = torch.randn(2, 22223, 256, device=DEV)
+    res = {}
+    for flag in (True, False):
+        wgrad.ENABLED = flag
+        castcache.clear()
+        lin.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = castcache.linear(xi, lin.weight, lin.bias)
+        (y.float() * gy).sum().backward()
+        res[flag] = (y.float(), lin.weight.grad.clone(), lin.bias.grad.clone(), xi.grad.clone())
+    wgrad.ENABLED = True
+    xd = x.double().requires_grad_(True)
+    wd = lin.weight.double().requires_grad_(True)
+    bd = lin.bias.double().requires_grad_(True)
+    yd = torch.nn.functional.linear(xd, wd, bd)
+    (yd * gy.double()).sum().backward()
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=0, atol=0)
+    for k, ref in ((1, wd.grad), (2, bd.grad), (3, xd.grad)):
+        mine = _rel(res[True][k].cpu(), ref.cpu())
+        lib = _rel(res[False][k].cpu(), ref.cpu())
+        assert mine < 1e-2 and mine <= lib * 1.5 + 1e-6, (k, mine, lib)
