@@ -55,6 +55,11 @@
  *                        nn.Linear layers (autograd's dW = dY^T X GEMM), as a
  *                        split-K fp32 reduction (no reference counterpart:
  *                        torch autograd in the reference)
+ *   gd_add_layernorm_forward / _backward / _workspace_bytes
+ *                     <- the post-norm `norm(src + dropout(src2))` of the
+ *                        deformable encoder / decoder layers and the text
+ *                        enhancer (transformer.py:789-808, 877-936,
+ *                        transformer_vanilla.py:83-110) and its backward
  *   gd_contrastive_forward
  *                     <- ContrastiveEmbed.forward (x . text^T, -inf on padded
  *                        tokens, -inf right padding to max_text_len)
@@ -282,6 +287,27 @@ size_t gd_wgrad_workspace_bytes(int O, int I, int splits);
 gd_status gd_wgrad(gd_dtype dtype, const void* grad_y, int64_t ldy, const void* x, int64_t ldx, int T,
                    int O, int I, int splits, void* workspace, float* grad_w, float* grad_b,
                    gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Residual add + LayerNorm                                                  */
+/* ------------------------------------------------------------------------ */
+/*
+ * x, r [rows, C] (F32 or BF16 each; r may be NULL), weight / bias [C] F32,
+ * C in {64, 128, 192, 256, 384, 512, 768, 1024}.
+ * y [rows, C] F32 = LayerNorm(x + r) * weight + bias; mean / rstd [rows] F32.
+ * Backward: grad_y F32 -> grad_x (x dtype), grad_r (r dtype, or NULL),
+ * grad_weight / grad_bias [C] F32 (both or neither; overwritten, need
+ * gd_add_layernorm_workspace_bytes(C) bytes of workspace).  Deterministic.
+ */
+size_t gd_add_layernorm_workspace_bytes(int C);
+gd_status gd_add_layernorm_forward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                   const float* weight, const float* bias, int64_t rows, int C,
+                                   float eps, float* y, float* mean, float* rstd, gd_stream_t stream);
+gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                    const float* weight, const float* grad_y, const float* mean,
+                                    const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,
+                                    float* grad_weight, float* grad_bias, void* workspace,
+                                    gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

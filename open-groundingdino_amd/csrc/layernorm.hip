@@ -1,0 +1,262 @@
+// Residual add + LayerNorm for gfx950: the post-norm sublayer ending
+//   y = LayerNorm(x + r) * w + b
+// of the deformable encoder / decoder layers and the text enhancer
+// (reference transformer.py:789-808, 877-936, transformer_vanilla.py:83-110:
+// `norm(src + dropout(src2))`).  Under bf16 autocast the reference runs an
+// fp32 add of the bf16 sublayer output into the fp32 residual stream, then
+// PyTorch's LayerNorm (fp32), and in the backward the LayerNorm input
+// gradient, the gamma / beta partial sums and a bf16 cast of the gradient
+// sent to the sublayer.  Here: one kernel forward (s = x + r, mean / rstd,
+// y), one kernel backward (ds, dx = ds, dr = ds in r's dtype, per-wave
+// gamma / beta partials) and a column reduction of the partials.
+//
+// One wave per row (grid-stride over rows); lane j owns columns j + 64e,
+// e < E = C / 64, so every access is a coalesced 256-B (fp32) row segment and
+// the row statistics are wave shuffles.  The variance is the two-pass
+// mean((s - mean)^2) over the registers.  s is recomputed from x and r in the
+// backward instead of being stored.
+#include "gd_common.h"
+
+#include <cmath>
+#include <type_traits>
+
+namespace gd {
+namespace {
+
+template <typename T> __device__ __forceinline__ float ldv(const T* p);
+template <> __device__ __forceinline__ float ldv<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ldv<uint16_t>(const uint16_t* p) { return bf16_to_f32(*p); }
+template <typename T> __device__ __forceinline__ void stv(T* p, float v);
+template <> __device__ __forceinline__ void stv<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void stv<uint16_t>(uint16_t* p, float v) { *p = f32_to_bf16(v); }
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// grid-stride: wave w of the grid handles rows w, w + nwaves, ...
+template <typename TX, typename TR, int E>
+__global__ void __launch_bounds__(256)
+addln_fwd_kernel(const TX* __restrict__ x, const TR* __restrict__ r, const float* __restrict__ w,
+                 const float* __restrict__ b, int64_t rows, float eps, float* __restrict__ y,
+                 float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int C = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  float wv[E], bv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    wv[e] = w ? w[lane + 64 * e] : 1.f;
+    bv[e] = b ? b[lane + 64 * e] : 0.f;
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    float s[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      s[e] = ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) sum += s[e];
+    const float mean = wsum(sum) / float(C);
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float d = s[e] - mean;
+      sq += d * d;
+    }
+    const float rstd = rsqrtf(wsum(sq) / float(C) + eps);
+#pragma unroll
+    for (int e = 0; e < E; ++e) y[row * C + lane + 64 * e] = (s[e] - mean) * rstd * wv[e] + bv[e];
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// dy [rows, C] fp32 -> dx (TX), dr (TR, optional), partial dw / db per wave
+template <typename TX, typename TR, int E>
+__global__ void __launch_bounds__(256)
+addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const TR* __restrict__ r,
+                 const float* __restrict__ w, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                 int64_t rows, TX* __restrict__ dx, TR* __restrict__ dr, float* __restrict__ part_w,
+                 float* __restrict__ part_b) {
+  constexpr int C = 64 * E;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  float wv[E], gw[E], gb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    wv[e] = w ? w[lane + 64 * e] : 1.f;
+    gw[e] = gb[e] = 0.f;
+  }
+  for (int64_t row = wave_id; row < rows; row += nwaves) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[E], g[E];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      const float s = ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f);
+      xh[e] = (s - mean) * rstd;
+      const float d = dy[o];
+      gw[e] += d * xh[e];
+      gb[e] += d;
+      g[e] = d * wv[e];
+      sg += g[e];
+      sgx += g[e] * xh[e];
+    }
+    const float mg = wsum(sg) / float(C), mgx = wsum(sgx) / float(C);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      const float ds = rstd * (g[e] - mg - xh[e] * mgx);
+      stv<TX>(dx + o, ds);
+      if (dr) stv<TR>(dr + o, ds);
+    }
+  }
+  if (part_w) {  // combine the block's 4 waves in LDS: one partial row per block
+    __shared__ float red[2][4][C];
+    const int wv_i = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      red[0][wv_i][lane + 64 * e] = gw[e];
+      red[1][wv_i][lane + 64 * e] = gb[e];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      part_w[int64_t(blockIdx.x) * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+      part_b[int64_t(blockIdx.x) * C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    }
+  }
+}
+
+// dw[c] = sum_k part_w[k][c], db likewise; grid ceil(C / 64), block 1024 =
+// 64 columns x 16 row groups, combined through LDS (fixed order:
+// deterministic)
+__global__ void __launch_bounds__(1024)
+addln_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ part_b, int nparts, int C,
+                    float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[2][16][64];
+  const int cx = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  float sw = 0.f, sb = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = grp; k < nparts; k += 16) {
+      sw += part_w[int64_t(k) * C + c];
+      sb += part_b[int64_t(k) * C + c];
+    }
+  }
+  red[0][grp][cx] = sw;
+  red[1][grp][cx] = sb;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      sw += red[0][k][cx];
+      sb += red[1][k][cx];
+    }
+    dw[c] = sw;
+    db[c] = sb;
+  }
+}
+
+constexpr int kLnBlocks = 512;  // backward grid: 2048 waves, one partial row per block
+
+template <typename Fn>
+gd_status dispatch_types(gd_dtype tx, gd_dtype tr, bool has_r, int C, Fn&& fn) {
+  GD_REQUIRE(tx == GD_F32 || tx == GD_BF16, "add_layernorm: x dtype %d (F32, BF16)", int(tx));
+  GD_REQUIRE(!has_r || tr == GD_F32 || tr == GD_BF16, "add_layernorm: r dtype %d (F32, BF16)", int(tr));
+  GD_REQUIRE(C == 64 || C == 128 || C == 192 || C == 256 || C == 384 || C == 512 || C == 768 || C == 1024,
+             "add_layernorm: C=%d not supported (64, 128, 192, 256, 384, 512, 768, 1024)", C);
+  auto with_e = [&](auto tx_tag, auto tr_tag) {
+    using TX = decltype(tx_tag);
+    using TR = decltype(tr_tag);
+    switch (C) {
+      case 64: fn(TX{}, TR{}, std::integral_constant<int, 1>{}); break;
+      case 128: fn(TX{}, TR{}, std::integral_constant<int, 2>{}); break;
+      case 192: fn(TX{}, TR{}, std::integral_constant<int, 3>{}); break;
+      case 256: fn(TX{}, TR{}, std::integral_constant<int, 4>{}); break;
+      case 384: fn(TX{}, TR{}, std::integral_constant<int, 6>{}); break;
+      case 512: fn(TX{}, TR{}, std::integral_constant<int, 8>{}); break;
+      case 768: fn(TX{}, TR{}, std::integral_constant<int, 12>{}); break;
+      default: fn(TX{}, TR{}, std::integral_constant<int, 16>{}); break;
+    }
+  };
+  const bool xb = tx == GD_BF16, rb = has_r && tr == GD_BF16;
+  if (xb && rb) with_e(uint16_t{}, uint16_t{});
+  else if (xb) with_e(uint16_t{}, float{});
+  else if (rb) with_e(float{}, uint16_t{});
+  else with_e(float{}, float{});
+  return GD_OK;
+}
+
+}  // namespace
+}  // namespace gd
+
+using namespace gd;
+
+extern "C" size_t gd_add_layernorm_workspace_bytes(int C) { return sizeof(float) * size_t(kLnBlocks) * C * 2; }
+
+extern "C" gd_status gd_add_layernorm_forward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                             const float* weight, const float* bias, int64_t rows, int C,
+                                             float eps, float* y, float* mean, float* rstd, gd_stream_t stream) {
+  GD_REQUIRE(rows >= 0, "add_layernorm: rows < 0");
+  if (rows == 0) return gd_status(GD_OK);
+  GD_REQUIRE(x && y && mean && rstd, "add_layernorm_forward: null pointer");
+  hipStream_t s = as_hip(stream);
+  const int64_t blocks64 = (rows + 3) / 4;
+  const unsigned blocks = unsigned(blocks64 < 8192 ? blocks64 : 8192);
+  gd_status st = dispatch_types(x_dtype, r_dtype, r != nullptr, C, [&](auto tx, auto tr, auto e) {
+    using TX = decltype(tx);
+    using TR = decltype(tr);
+    hipLaunchKernelGGL((addln_fwd_kernel<TX, TR, decltype(e)::value>), dim3(blocks), dim3(256), 0, s,
+                       (const TX*)x, (const TR*)r, weight, bias, rows, eps, y, mean, rstd);
+  });
+  if (st != GD_OK) return st;
+  GD_LAUNCH_CHECK("add_layernorm_fwd");
+  return GD_OK;
+}
+
+extern "C" gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                              const float* weight, const float* grad_y, const float* mean,
+                                              const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,
+                                              float* grad_weight, float* grad_bias, void* workspace,
+                                              gd_stream_t stream) {
+  GD_REQUIRE(rows >= 0, "add_layernorm: rows < 0");
+  GD_REQUIRE((grad_weight == nullptr) == (grad_bias == nullptr),
+             "add_layernorm_backward: grad_weight and grad_bias are requested together");
+  if (rows == 0) {
+    hipStream_t s = as_hip(stream);
+    if (grad_weight) GD_HIP_CHECK(hipMemsetAsync(grad_weight, 0, sizeof(float) * C, s));
+    if (grad_bias) GD_HIP_CHECK(hipMemsetAsync(grad_bias, 0, sizeof(float) * C, s));
+    return GD_OK;
+  }
+  GD_REQUIRE(x && grad_y && mean && rstd && grad_x, "add_layernorm_backward: null pointer");
+  GD_REQUIRE(!grad_r || r, "add_layernorm_backward: grad_r without r");
+  GD_REQUIRE(!grad_weight || workspace, "add_layernorm_backward: workspace missing");
+  hipStream_t s = as_hip(stream);
+  float* part_w = grad_weight ? static_cast<float*>(workspace) : nullptr;
+  float* part_b = grad_weight ? part_w + int64_t(kLnBlocks) * C : nullptr;
+  gd_status st = dispatch_types(x_dtype, r_dtype, r != nullptr, C, [&](auto tx, auto tr, auto e) {
+    using TX = decltype(tx);
+    using TR = decltype(tr);
+    hipLaunchKernelGGL((addln_bwd_kernel<TX, TR, decltype(e)::value>), dim3(kLnBlocks), dim3(256), 0, s, grad_y,
+                       (const TX*)x, (const TR*)r, weight, mean, rstd, rows, (TX*)grad_x, (TR*)grad_r, part_w,
+                       part_b);
+  });
+  if (st != GD_OK) return st;
+  GD_LAUNCH_CHECK("add_layernorm_bwd");
+  if (grad_weight) {
+    hipLaunchKernelGGL(addln_reduce_kernel, dim3(unsigned((C + 63) / 64)), dim3(1024), 0, s, part_w, part_b,
+                       kLnBlocks, C, grad_weight, grad_bias);
+    GD_LAUNCH_CHECK("add_layernorm_reduce");
+  }
+  return GD_OK;
+}

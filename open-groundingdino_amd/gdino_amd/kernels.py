@@ -152,3 +152,4 @@ from . import attn  # noqa: E402,F401
 from . import contrastive  # noqa: E402,F401
 from . import msda_prologue  # noqa: E402,F401
 from . import wgrad  # noqa: E402,F401
+from . import layernorm  # noqa: E402,F401

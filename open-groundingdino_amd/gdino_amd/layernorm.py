@@ -1,0 +1,84 @@
+"""Residual add + LayerNorm on MI355X (csrc/layernorm.hip).
+
+``add_norm(norm, x, r)`` = ``norm(x + r)`` for an nn.LayerNorm ``norm``: the
+post-norm sublayer ending of the deformable encoder / decoder layers and the
+text enhancer (reference transformer.py:789-808, 877-936,
+transformer_vanilla.py:83-110).  On the GPU it is one kernel forward (the add,
+the row statistics and the affine output in fp32, as autocast's fp32
+LayerNorm) and one kernel + a column reduction backward (the input gradient
+written once for the residual in x's dtype and once for the sublayer in r's
+dtype, gamma / beta gradients in fp32).  Elsewhere (CPU, other widths) it is
+the plain composition.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib
+
+_p, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+_lib.register("gd_add_layernorm_forward", [_i, _p, _i, _p, _p, _p, _i64, _i, _f, _p, _p, _p, _p])
+_lib.register("gd_add_layernorm_backward", [_i, _p, _i, _p, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p])
+
+WIDTHS = (64, 128, 192, 256, 384, 512, 768, 1024)
+ENABLED = True
+
+
+def supported(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor) -> bool:
+    c = x.shape[-1]
+    return (ENABLED and x.is_cuda and len(norm.normalized_shape) == 1 and norm.normalized_shape[0] == c
+            and c in WIDTHS and norm.elementwise_affine and norm.weight is not None and norm.bias is not None
+            and norm.weight.dtype == torch.float32 and norm.bias.dtype == torch.float32
+            and x.dtype in (torch.float32, torch.bfloat16) and r.dtype in (torch.float32, torch.bfloat16)
+            and x.shape == r.shape)
+
+
+def _workspace(c, device):
+    fn = _lib.lib().gd_add_layernorm_workspace_bytes
+    fn.restype, fn.argtypes = ctypes.c_size_t, [_i]
+    return torch.empty((int(fn(c)) + 3) // 4, dtype=torch.float32, device=device)
+
+
+class AddLayerNormFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps):
+        c = x.shape[-1]
+        rows = x.numel() // c
+        y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        _lib.call("gd_add_layernorm_forward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(r), r.data_ptr(),
+                  weight.data_ptr(), bias.data_ptr(), rows, c, float(eps), y.data_ptr(), mean.data_ptr(),
+                  rstd.data_ptr(), _lib.stream_of(x))
+        ctx.save_for_backward(x, r, weight, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, r, weight, mean, rstd = ctx.saved_tensors
+        c = x.shape[-1]
+        rows = x.numel() // c
+        dy = dy.float().contiguous()
+        dx = torch.empty_like(x)
+        dr = torch.empty_like(r) if ctx.needs_input_grad[1] else None
+        want_wb = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dw = torch.empty(c, dtype=torch.float32, device=x.device) if want_wb else None
+        db = torch.empty(c, dtype=torch.float32, device=x.device) if want_wb else None
+        ws = _workspace(c, x.device) if want_wb else None
+        _lib.call("gd_add_layernorm_backward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(r), r.data_ptr(),
+                  weight.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, c, dx.data_ptr(),
+                  _lib.ptr(dr), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws), _lib.stream_of(x))
+        return (dx if ctx.needs_input_grad[0] else None, dr, dw if ctx.needs_input_grad[2] else None,
+                db if ctx.needs_input_grad[3] else None, None)
+
+
+def add_norm(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """norm(x + r)"""
+    if supported(norm, x, r):
+        # (the decoder's MSDA output arrives transposed: one copy, which the
+        # unfused add would pay as well)
+        return AddLayerNormFunction.apply(x.contiguous(), r.contiguous(), norm.weight, norm.bias, norm.eps)
+    return norm(x + r)

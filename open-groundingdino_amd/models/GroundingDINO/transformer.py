@@ -22,6 +22,7 @@ import torch.utils.checkpoint as checkpoint
 from torch import Tensor, nn
 
 from gdino_amd import kernels
+from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
 from gdino_amd.misc import device_const, inverse_sigmoid
 
@@ -360,13 +361,13 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
-        return self.norm2(src + self.dropout3(src2))
+        return add_norm(self.norm2, src, self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, key_padding_mask=None):
         src2 = self.self_attn(query=self.with_pos_embed(src, pos), reference_points=reference_points, value=src,
                               spatial_shapes=spatial_shapes, level_start_index=level_start_index,
                               key_padding_mask=key_padding_mask)
-        src = self.norm1(src + self.dropout1(src2))
+        src = add_norm(self.norm1, src, self.dropout1(src2))
         return self.forward_ffn(src)
 
 
@@ -410,7 +411,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         with torch.autocast(device_type=tgt.device.type, enabled=False):
             t = tgt.float() if tgt.dtype in (torch.float16, torch.bfloat16) else tgt
             tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(t))))
-        return self.norm3(tgt + self.dropout4(tgt2))
+        return add_norm(self.norm3, tgt, self.dropout4(tgt2))
 
     def forward(self, tgt, tgt_query_pos=None, tgt_query_sine_embed=None, tgt_key_padding_mask=None,
                 tgt_reference_points=None, memory_text=None, text_attention_mask=None, memory=None,
@@ -420,7 +421,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         if self.self_attn is not None:
             q = k = self.with_pos_embed(tgt, tgt_query_pos)
             tgt2 = self.self_attn(q, k, tgt, attn_mask=self_attn_mask)[0]
-            tgt = self.norm2(tgt + self.dropout2(tgt2))
+            tgt = add_norm(self.norm2, tgt, self.dropout2(tgt2))
         if self.use_text_cross_attention:
             # key and value are the same tensor (reference :900-905 passes
             # two identical transposes): one object lets the MHA project them
@@ -428,13 +429,13 @@ class DeformableTransformerDecoderLayer(nn.Module):
             text_kv = memory_text.transpose(0, 1)
             tgt2 = self.ca_text(self.with_pos_embed(tgt, tgt_query_pos), text_kv, text_kv,
                                 key_padding_mask=text_attention_mask)[0]
-            tgt = self.catext_norm(tgt + self.catext_dropout(tgt2))
+            tgt = add_norm(self.catext_norm, tgt, self.catext_dropout(tgt2))
         tgt2 = self.cross_attn(query=self.with_pos_embed(tgt, tgt_query_pos).transpose(0, 1),
                                reference_points=tgt_reference_points.transpose(0, 1).contiguous(),
                                value=memory.transpose(0, 1), spatial_shapes=memory_spatial_shapes,
                                level_start_index=memory_level_start_index,
                                key_padding_mask=memory_key_padding_mask).transpose(0, 1)
-        tgt = self.norm1(tgt + self.dropout1(tgt2))
+        tgt = add_norm(self.norm1, tgt, self.dropout1(tgt2))
         return self.forward_ffn(tgt)
 
 

@@ -6,6 +6,7 @@ from typing import Optional
 import torch
 from torch import Tensor, nn
 
+from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
 
 from .utils import _get_activation_fn, _get_clones
@@ -39,9 +40,9 @@ class TransformerEncoderLayer(nn.Module):
             src_mask = src_mask.repeat(self.nhead, 1, 1)
         qk = src if pos is None else src + pos
         attn = self.self_attn(qk, qk, value=src, attn_mask=src_mask)[0]
-        src = self.norm1(src + self.dropout1(attn))
+        src = add_norm(self.norm1, src, self.dropout1(attn))
         ffn = self.linear2(self.dropout(self.activation(self.linear1(src))))
-        return self.norm2(src + self.dropout2(ffn))
+        return add_norm(self.norm2, src, self.dropout2(ffn))
 
 
 class TextTransformer(nn.Module):

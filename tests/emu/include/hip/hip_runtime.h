@@ -62,6 +62,7 @@ inline uint2 make_uint2(unsigned a, unsigned b) { return {a, b}; }
 inline uint4 make_uint4(unsigned a, unsigned b, unsigned c, unsigned d) { return {a, b, c, d}; }
 inline float __logf(float x) { return logf(x); }
 inline float __fadd_rn(float a, float b) { return a + b; }
+inline float rsqrtf(float x) { return 1.0f / sqrtf(x); }
 inline float __fmul_rn(float a, float b) { return a * b; }
 inline float __fdiv_rn(float a, float b) { return a / b; }
 

@@ -48,6 +48,10 @@ def lib():
         _LIB.gd_wgrad_splits.argtypes = [_i, _i, _i]
         _LIB.gd_wgrad_workspace_bytes.argtypes = [_i, _i, _i]
         _LIB.gd_wgrad_workspace_bytes.restype = ctypes.c_size_t
+        _LIB.gd_add_layernorm_forward.argtypes = [_i, _p, _i, _p, _p, _p, _i64, _i, ctypes.c_float, _p, _p, _p, _p]
+        _LIB.gd_add_layernorm_backward.argtypes = [_i, _p, _i, _p, _p, _p, _p, _p, _i64, _i] + [_p] * 6
+        _LIB.gd_add_layernorm_workspace_bytes.argtypes = [_i]
+        _LIB.gd_add_layernorm_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_last_error.restype = ctypes.c_char_p
         _LIB.gd_runtime_info.restype = ctypes.c_char_p
     return _LIB
@@ -257,6 +261,31 @@ def wgrad(dy, x, bias=True, splits=None):
     _check(lib().gd_wgrad(_code(dy), _ptr(dy), dy.stride(0), _ptr(x), x.stride(0), T, O, I, s, _ptr(ws), _ptr(dw),
                           _ptr(db), None))
     return dw, db
+
+
+def add_layernorm_forward(x, r, w, b, eps):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    y = torch.full(x.shape, float("nan"))
+    mean = torch.full((rows,), float("nan"))
+    rstd = torch.full((rows,), float("nan"))
+    _check(lib().gd_add_layernorm_forward(_code(x), _ptr(x), _code(r) if r is not None else 0, _ptr(r), _ptr(w),
+                                          _ptr(b), rows, C, eps, _ptr(y), _ptr(mean), _ptr(rstd), None))
+    return y, mean, rstd
+
+
+def add_layernorm_backward(x, r, w, dy, mean, rstd):
+    C = x.shape[-1]
+    rows = x.numel() // C
+    dx = torch.full_like(x, float("nan"))
+    dr = None if r is None else torch.full_like(r, float("nan"))
+    dw = torch.full((C,), float("nan"))
+    db = torch.full((C,), float("nan"))
+    ws = torch.empty((int(lib().gd_add_layernorm_workspace_bytes(C)) + 3) // 4)
+    _check(lib().gd_add_layernorm_backward(_code(x), _ptr(x), _code(r) if r is not None else 0, _ptr(r), _ptr(w),
+                                           _ptr(dy.contiguous()), _ptr(mean), _ptr(rstd), rows, C, _ptr(dx),
+                                           _ptr(dr), _ptr(dw), _ptr(db), _ptr(ws), None))
+    return dx, dr, dw, db
 
 
 def attn_dropout_keep(B, H, Lq, Lk, p, seed):

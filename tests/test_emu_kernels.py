@@ -473,3 +473,31 @@ def test_emulated_wgrad(T, O, I, splits, dtype, tol):
     assert E.rel_err(db, ref_b) < tol * 10
     dw2, none = E.wgrad(dy, x, bias=False, splits=splits)
     assert none is None and torch.equal(dw, dw2)
+
+
+# ------------------------------------------------ residual add + LayerNorm
+@pytest.mark.parametrize("rows,C,xd,rd", [
+    (37, 256, torch.float32, torch.bfloat16),   # fp32 residual + bf16 sublayer output (autocast)
+    (50, 192, torch.float32, torch.float32),
+    (9, 768, torch.bfloat16, torch.bfloat16),
+    (3000, 64, torch.float32, torch.float32),   # more rows than the backward grid's waves
+])
+def test_emulated_add_layernorm(rows, C, xd, rd):
+    g = torch.Generator().manual_seed(rows + C)
+    x = (torch.randn(rows, C, generator=g) * 2 + 0.5).to(xd)
+    r = torch.randn(rows, C, generator=g).to(rd)
+    w = torch.randn(C, generator=g)
+    b = torch.randn(C, generator=g)
+    y, mean, rstd = E.add_layernorm_forward(x, r, w, b, 1e-5)
+    xs = (x.double() + r.double()).requires_grad_(True)
+    wd, bd = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xs, (C,), wd, bd, 1e-5)
+    assert E.rel_err(y, ref.detach()) < 1e-5
+    dy = torch.randn(rows, C, generator=g)
+    ref.backward(dy.double())
+    dx, dr, dw, db = E.add_layernorm_backward(x, r, w, dy, mean, rstd)
+    tol = 1e-5 if xd == torch.float32 else 1e-2
+    assert E.rel_err(dx.double(), xs.grad) < tol
+    assert E.rel_err(dr.double(), xs.grad) < (1e-5 if rd == torch.float32 else 1e-2)
+    assert E.rel_err(dw, wd.grad) < 1e-5
+    assert E.rel_err(db, bd.grad) < 1e-5

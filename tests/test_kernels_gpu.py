@@ -316,3 +316,35 @@ def test_token_linear_matches_autocast_linear():
         mine = _rel(res[True][k].cpu(), ref.cpu())
         lib = _rel(res[False][k].cpu(), ref.cpu())
         assert mine < 1e-2 and mine <= lib * 1.5 + 1e-6, (k, mine, lib)
+
+
+# ------------------------------------------- residual add + LayerNorm (HIP)
+@pytest.mark.parametrize("shape,xd,rd", [((2, 22223, 256), torch.float32, torch.bfloat16),   # encoder, autocast
+                                         ((900, 2, 256), torch.float32, torch.bfloat16),     # decoder (seq-first)
+                                         ((2, 256, 256), torch.float32, torch.float32)])
+def test_add_layernorm_matches_reference(shape, xd, rd):
+    from gdino_amd.layernorm import AddLayerNormFunction, add_norm
+    g = torch.Generator().manual_seed(shape[1])
+    c = shape[-1]
+    norm = torch.nn.LayerNorm(c).to(DEV)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(c, generator=g))
+        norm.bias.copy_(torch.randn(c, generator=g))
+    x = (torch.randn(shape, generator=g) * 2).to(xd)
+    r = torch.randn(shape, generator=g).to(rd)
+    dy = torch.randn(shape, generator=g)
+    xg, rg = x.to(DEV).requires_grad_(True), r.to(DEV).requires_grad_(True)
+    y = add_norm(norm, xg, rg)
+    assert y.grad_fn is not None and "AddLayerNorm" in type(y.grad_fn).__name__
+    y.backward(dy.to(DEV))
+    xd64 = x.double().requires_grad_(True)
+    rd64 = r.double().requires_grad_(True)
+    wd = norm.weight.detach().double().cpu().requires_grad_(True)
+    bd = norm.bias.detach().double().cpu().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xd64 + rd64, (c,), wd, bd, norm.eps)
+    ref.backward(dy.double())
+    assert _rel(y.detach().cpu(), ref.detach()) < 1e-5
+    assert _rel(xg.grad.cpu(), xd64.grad) < 1e-5
+    assert _rel(rg.grad.cpu(), rd64.grad) < (1e-2 if rd == torch.bfloat16 else 1e-5)
+    assert _rel(norm.weight.grad.cpu(), wd.grad) < 1e-5
+    assert _rel(norm.bias.grad.cpu(), bd.grad) < 1e-5
