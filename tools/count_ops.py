@@ -57,7 +57,7 @@ class Counter(TorchDispatchMode):
                 self.counts[name] += 1
                 self.by_phase[self.phase] += 1
                 self.phase_ops[self.phase][name] += 1
-                if self.where is not None and self.phase in ("forward", "criterion") and (
+                if self.where is not None and self.phase in ("forward", "criterion", "backward") and (
                         not _OP_FILTER or any(f in name for f in _OP_FILTER)):
                     import traceback
                     for fr in reversed(traceback.extract_stack()[:-1]):
@@ -178,6 +178,20 @@ def main():
         def apply(*x):
             return pro_op(*x)
 
+    # residual add + LayerNorm (GPU-only, gdino_amd/layernorm.py): one
+    # launch forward, two backward (kernel + column reduction)
+    from gdino_amd import layernorm as ln_mod
+    ln_op = counted(lambda x, r, w, b, eps: torch.nn.functional.layer_norm(x.float() + r.float(), w.shape, w, b, eps),
+                    "gd.add_layernorm")
+
+    class CountedAddLN:
+        @staticmethod
+        def apply(*x):
+            return ln_op(*x)
+
+    prev_ln = (ln_mod.supported, ln_mod.AddLayerNormFunction)
+    ln_mod.supported = lambda norm, x, r: x.shape[-1] in ln_mod.WIDTHS and norm.elementwise_affine
+    ln_mod.AddLayerNormFunction = CountedAddLN
     prev_pro = (pro_mod.supported, pro_mod.MSDAPrologue)
     pro_mod.supported = lambda off, logit, ref, l, p: l * p == 16 and not ref.requires_grad
     pro_mod.MSDAPrologue = CountedPrologue
@@ -216,6 +230,7 @@ def main():
     finally:
         msda_mod.MSDeformAttnFunction = prev
         pro_mod.supported, pro_mod.MSDAPrologue = prev_pro
+        ln_mod.supported, ln_mod.AddLayerNormFunction = prev_ln
     total = sum(counter.counts.values())
     casts = sum(v for k, v in counter.counts.items() if k.startswith("aten._to_copy"))
     print(f"dispatches/step={total} (+~25 fused AdamW on GPU)  casts={casts}  by phase: {dict(counter.by_phase)}")
