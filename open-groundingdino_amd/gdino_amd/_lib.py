@@ -9,6 +9,7 @@ whose CPU backend raises "Not implemented on the CPU"
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 import threading
 
@@ -122,6 +123,21 @@ def require_contiguous(what: str, **tensors: torch.Tensor) -> None:
     for name, t in tensors.items():
         if t is not None and not t.is_contiguous():
             raise RuntimeError(f"{name} tensor has to be contiguous ({what})")
+
+
+@functools.lru_cache(maxsize=8)
+def _disabled(spec: str) -> frozenset:
+    return frozenset(x.strip() for x in spec.split(",") if x.strip())
+
+
+def enabled(family: str) -> bool:
+    """False when ``family`` is listed in GDINO_DISABLE (comma-separated:
+    wattn, attn, contrastive, prologue, wgrad, addln).  A disabled family runs
+    its torch composition (ROCm library kernels) instead -- for A/B runs and
+    bisection on the box; the MSDA core and BiAttention kernels have no such
+    switch (GD_MSDA_BWD=lane32 selects the round-1 MSDA backward)."""
+    spec = os.environ.get("GDINO_DISABLE")
+    return not spec or family not in _disabled(spec)
 
 
 def ptr(t) -> int | None:

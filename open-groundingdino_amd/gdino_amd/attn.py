@@ -70,7 +70,7 @@ def _mask_args(mask, b, h, lq, lk):
 
 def supported(q, k, v, dropout_p) -> bool:
     hd = q.shape[-1]
-    return (0.0 <= dropout_p < 1.0 and q.dtype in (torch.float32, torch.bfloat16) and q.dtype == k.dtype == v.dtype
+    return (_lib.enabled("attn") and 0.0 <= dropout_p < 1.0 and q.dtype in (torch.float32, torch.bfloat16) and q.dtype == k.dtype == v.dtype
             and hd in (32, 64) and k.shape[-1] == hd and v.shape[-1] == hd and q.shape[2] > 0 and k.shape[2] > 0
             and q.shape[0] * q.shape[1] < 65536)
 

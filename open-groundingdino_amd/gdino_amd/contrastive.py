@@ -57,7 +57,7 @@ def _launch(xc, tc, keep, tout, logits, rowmax):
 
 
 def supported(x, text, max_text_len) -> bool:
-    return (x.dim() == 3 and text.dim() == 3 and x.shape[-1] == text.shape[-1] and x.shape[-1] % 32 == 0
+    return (_lib.enabled("contrastive") and x.dim() == 3 and text.dim() == 3 and x.shape[-1] == text.shape[-1] and x.shape[-1] % 32 == 0
             and 0 < text.shape[1] <= max_text_len and x.shape[0] < 65536)
 
 

@@ -39,7 +39,7 @@ MAX_TOKENS = 64
 
 def supported(qkv: torch.Tensor) -> bool:
     _, n, _, _, hd = qkv.shape
-    return qkv.dtype in (torch.float32, torch.bfloat16) and n <= MAX_TOKENS and hd == 32
+    return _lib.enabled("wattn") and qkv.dtype in (torch.float32, torch.bfloat16) and n <= MAX_TOKENS and hd == 32
 
 
 class WindowAttnFunction(torch.autograd.Function):

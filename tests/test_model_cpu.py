@@ -229,3 +229,13 @@ def test_window_attention_packed_torch_composition_matches_oracle():
         torch.testing.assert_close(window_attention_packed_torch(qkv, table, ridx, mask, 32 ** -0.5),
                                    window_attention_packed_ref(qkv, table, ridx, mask, 32 ** -0.5),
                                    rtol=1e-12, atol=1e-12)
+
+
+def test_kernel_families_can_be_disabled(monkeypatch):
+    """GDINO_DISABLE lists kernel families that fall back to their torch
+    compositions (A/B runs and bisection on the box)."""
+    from gdino_amd import _lib
+    monkeypatch.setenv("GDINO_DISABLE", "wattn, attn")
+    assert not _lib.enabled("wattn") and not _lib.enabled("attn") and _lib.enabled("addln")
+    monkeypatch.delenv("GDINO_DISABLE")
+    assert _lib.enabled("wattn")
