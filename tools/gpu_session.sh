@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # One GPU session on a fresh MI355X box (run through gpurun from the repo root):
-#   gpurun --timeout 1200 -- bash tools/gpu_session.sh [core|tune|graphs]
+#   gpurun --timeout 1200 -- bash tools/gpu_session.sh [core|ab|tune|graphs]
 # Every GPU step has its own time limit and the steps are chained with &&:
 # the first failure ends the session (no retries, no further GPU work).
 # Logs and profiler output go to gpurun_out/ (copy the summaries that are to
@@ -39,6 +39,17 @@ tune)
   T 600 python3 bench.py --no-cpu-baseline --tunableop tunableop/gdino_train_gfx950.csv \
       > gpurun_out/s_bench_tunable.log 2>&1
   ;;
+ab)
+  # A/B of every kernel family against its torch composition (GDINO_DISABLE)
+  # and of the MSDA backward against the round-1 kernel: one bench line each
+  T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_ab_all.log 2>&1 &&
+  for fam in wattn attn contrastive prologue wgrad addln; do
+    GDINO_DISABLE=$fam T 600 python3 bench.py --no-cpu-baseline > "gpurun_out/s_ab_no_$fam.log" 2>&1 || exit $?
+  done &&
+  GD_MSDA_BWD=lane32 T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_ab_msda_lane32.log 2>&1 &&
+  GDINO_DISABLE=wattn,attn,contrastive,prologue,wgrad,addln T 600 python3 bench.py --no-cpu-baseline \
+      > gpurun_out/s_ab_none.log 2>&1
+  ;;
 graphs)
   # HIP-graph replay (experimental; faulted in round 1 before MIOpen was
   # removed from the captured region): run alone, in its own gpurun call
@@ -46,7 +57,7 @@ graphs)
       > gpurun_out/s_bench_graphs.log 2>&1
   ;;
 *)
-  echo "usage: $0 [core|tune|graphs]" >&2
+  echo "usage: $0 [core|ab|tune|graphs]" >&2
   exit 2
   ;;
 esac
