@@ -111,11 +111,16 @@ def stream_of(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def on_device(t: torch.Tensor) -> bool:
+    """Whether t lives where the HIP library operates (a ROCm device)."""
+    return t.is_cuda
+
+
 def require_device(*tensors: torch.Tensor, what: str = "op") -> None:
     for t in tensors:
         if t is None:
             continue
-        if not t.is_cuda:
+        if not on_device(t):
             raise RuntimeError(f"gdino_amd {what}: Not implemented on the CPU (tensor on {t.device})")
 
 

@@ -29,8 +29,9 @@ _lib.register("gd_contrastive_forward", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i,
 
 
 def _compute_dtype(x, text):
-    if x.is_cuda and torch.is_autocast_enabled("cuda"):
-        return torch.get_autocast_dtype("cuda")
+    dev = x.device.type
+    if dev in ("cuda", "cpu") and torch.is_autocast_enabled(dev):
+        return torch.get_autocast_dtype(dev)
     return x.dtype if x.dtype == text.dtype else torch.float32
 
 

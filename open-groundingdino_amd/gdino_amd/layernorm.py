@@ -29,8 +29,8 @@ ENABLED = True
 
 def supported(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor) -> bool:
     c = x.shape[-1]
-    return (ENABLED and _lib.enabled("addln") and x.is_cuda and len(norm.normalized_shape) == 1 and norm.normalized_shape[0] == c
-            and c in WIDTHS and norm.elementwise_affine and norm.weight is not None and norm.bias is not None
+    return (ENABLED and _lib.enabled("addln") and _lib.on_device(x) and len(norm.normalized_shape) == 1
+            and norm.normalized_shape[0] == c and c in WIDTHS and norm.elementwise_affine and norm.weight is not None and norm.bias is not None
             and norm.weight.dtype == torch.float32 and norm.bias.dtype == torch.float32
             and x.dtype in (torch.float32, torch.bfloat16) and r.dtype in (torch.float32, torch.bfloat16)
             and x.shape == r.shape)

@@ -29,8 +29,8 @@ def _rows_ok(t):
 
 
 def supported(offsets, logits, reference_points, num_levels, num_points) -> bool:
-    return (_lib.enabled("prologue") and offsets.is_cuda and num_levels * num_points == 16 and offsets.dtype in (torch.float32, torch.bfloat16)
-            and logits.dtype == offsets.dtype and _rows_ok(offsets) and _rows_ok(logits)
+    return (_lib.enabled("prologue") and _lib.on_device(offsets) and num_levels * num_points == 16
+            and offsets.dtype in (torch.float32, torch.bfloat16) and logits.dtype == offsets.dtype and _rows_ok(offsets) and _rows_ok(logits)
             and reference_points.shape[-1] in (2, 4) and not reference_points.requires_grad)
 
 

@@ -34,7 +34,8 @@ ENABLED = True
 
 def eligible(x: torch.Tensor, out_features: int) -> bool:
     in_features = x.shape[-1]
-    if not (ENABLED and _lib.enabled("wgrad") and x.is_cuda and out_features % 64 == 0 and in_features % 64 == 0):
+    if not (ENABLED and _lib.enabled("wgrad") and _lib.on_device(x) and out_features % 64 == 0
+            and in_features % 64 == 0):
         return False
     tokens = x.numel() // max(in_features, 1)
     return tokens >= MIN_TOKENS and (out_features // 64) * (in_features // 64) <= MAX_TILES

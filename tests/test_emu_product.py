@@ -1,0 +1,119 @@
+"""The product's HIP path end to end on the CPU: one Grounding DINO train
+step (forward, criterion, backward) with every HIP op of the model reaching
+the host-side SIMT emulator build of the kernel sources through the
+product's own autograd functions and ctypes calls (tests/emu_product.py),
+against the same step with the ops routed to the oracle restatements
+(tests/oracle_hooks.py, pinned by the reference goldens).
+
+fp32, eval mode (no dropout / drop-path randomness): loss, logits and every
+parameter gradient agree to fp32 rounding.  Under bf16 autocast the
+two-stage top-k and the Hungarian matching are discrete, so the bf16 check
+compares the continuous part (backbone features, encoder memory) and the
+TokenLinear weight-gradient path in isolation.
+"""
+import pytest
+import torch
+
+import emu_product
+import oracle_hooks
+
+
+def _step(mode, amp, hooks=None, size=(96, 128)):
+    from gdino_amd import castcache, train
+    from gdino_amd.config import make_args
+    torch.manual_seed(0)
+    args = make_args(device="cpu", num_queries=100)
+    model, criterion, _, _ = train.build_training(args, "cpu")
+    model.eval()
+    samples, targets, captions, cats = train.synthetic_batch(1, size[0], size[1], n_boxes=3, n_tokens=24, seed=0,
+                                                             device="cpu")
+    captured = {}
+    handles = []
+    for name in hooks or ():
+        mod = dict(model.named_modules())[name]
+        handles.append(mod.register_forward_hook(
+            lambda m, i, o, name=name: captured.__setitem__(name, o)))
+    castcache.clear()
+    ctx = oracle_hooks.oracle_msda() if mode == "oracle" else emu_product.emulated_product(min_tokens=64)
+    try:
+        with ctx:
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=amp):
+                out = model(samples, captions=captions)
+                ld = criterion(out, targets, cats, captions)
+                loss = sum(ld[k] * criterion.weight_dict[k] for k in ld if k in criterion.weight_dict)
+            if not amp:
+                loss.backward()
+    finally:
+        for h in handles:
+            h.remove()
+    grads = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+    return loss.detach(), out["pred_logits"].detach(), grads, captured
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+@pytest.mark.slow
+def test_train_step_fp32_emulated_hip_path_matches_oracle_path():
+    lo, po, go, _ = _step("oracle", False)
+    le, pe, ge, _ = _step("emu", False)
+    assert abs(float(le - lo)) <= 1e-5 * abs(float(lo))
+    fin = torch.isfinite(po)
+    assert torch.equal(fin, torch.isfinite(pe))
+    assert _rel(pe[fin], po[fin]) < 1e-5
+    assert set(go) == set(ge)
+    worst = max((_rel(ge[n], go[n]), n) for n in go if go[n].norm() > 0)
+    assert worst[0] < 1e-4, worst
+
+
+def _flat(o):
+    if torch.is_tensor(o):
+        return [o]
+    if isinstance(o, dict):
+        return [t for v in o.values() for t in _flat(v)]
+    if isinstance(o, (list, tuple)):
+        return [t for v in o for t in _flat(v)]
+    return [t for t in (getattr(o, "tensors", None),) if t is not None]
+
+
+@pytest.mark.slow
+def test_forward_bf16_emulated_hip_path_matches_oracle_path():
+    names = ("backbone", "transformer.encoder")
+    _, _, _, co = _step("oracle", True, hooks=names)
+    _, _, _, ce = _step("emu", True, hooks=names)
+    for n in names:
+        for a, b in zip(_flat(ce[n]), _flat(co[n])):
+            if a.is_floating_point():
+                assert _rel(a.float(), b.float()) < 3e-2, n
+
+
+def test_token_linear_emulated_matches_library_linear():
+    """castcache.linear under bf16 autocast routed through TokenLinear (the
+    split-K weight-gradient kernel) vs the plain autocast F.linear path."""
+    from gdino_amd import castcache, wgrad
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(128, 192)
+    x = torch.randn(3, 300, 128)
+    gy = torch.randn(3, 300, 192)
+    res = {}
+    for use in (True, False):
+        castcache.clear()
+        lin.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with emu_product.emulated_product(min_tokens=64):
+            wgrad.ENABLED = use
+            try:
+                with torch.autocast("cpu", dtype=torch.bfloat16):
+                    y = castcache.linear(xi, lin.weight, lin.bias)
+                assert ("TokenLinear" in type(y.grad_fn).__name__) == use
+                (y.float() * gy).sum().backward()
+            finally:
+                wgrad.ENABLED = True
+        res[use] = (y.float(), lin.weight.grad.clone(), lin.bias.grad.clone(), xi.grad.clone())
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=0, atol=0)
+    xd, wd, bd = (t.double().requires_grad_(True) for t in (x, lin.weight.detach(), lin.bias.detach()))
+    (torch.nn.functional.linear(xd, wd, bd) * gy.double()).sum().backward()
+    for k, ref in ((1, wd.grad), (2, bd.grad), (3, xd.grad)):
+        assert _rel(res[True][k], ref) < 1e-2
+        assert _rel(res[True][k], ref) <= _rel(res[False][k], ref) * 1.5 + 1e-6, k
