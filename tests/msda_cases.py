@@ -45,3 +45,24 @@ def edge_excluded_mask(case):
         x = loc[:, :, :, lvl, :, 0] * w - 0.5
         mask[:, :, :, lvl, :] = (y == -1) | (x == -1) | (y == h) | (x == w) | (y == np.floor(y)) | (x == np.floor(x))
     return mask
+
+
+def smooth_samples(loc, shapes, eps=1e-4):
+    """[N, Lq, M, L, P, 1] bool: samples whose pixel coordinates are more than
+    eps from a cell edge.  grad_loc (the derivative of the bilinear
+    interpolation) jumps across cell edges, and fp32 vs fp64 rounding of
+    loc * size - 0.5 may put a sample on different sides of one; grad_value
+    and grad_attn are continuous there."""
+    loc = torch.as_tensor(loc).double().cpu()
+    hw = torch.as_tensor(shapes).double().cpu()  # [L, 2] (H, W)
+    w_im = loc[..., 0] * hw[:, 1][None, None, None, :, None] - 0.5
+    h_im = loc[..., 1] * hw[:, 0][None, None, None, :, None] - 0.5
+    ok = ((w_im - w_im.round()).abs() > eps) & ((h_im - h_im.round()).abs() > eps)
+    return ok[..., None].numpy()
+
+
+def rel_err_grad_loc(gl, ref_gl, loc, shapes):
+    keep = np.broadcast_to(smooth_samples(loc, shapes), np.shape(ref_gl))
+    a = np.asarray(gl, np.float64)[keep]
+    b = np.asarray(ref_gl, np.float64)[keep]
+    return float(np.abs(a - b).max() / max(np.abs(np.asarray(ref_gl, np.float64)).max(), 1e-30))

@@ -59,10 +59,11 @@ def _oracle_bwd(value, shapes, lsi, loc, attn, grad_out):
 
 
 def _check_bwd(inputs, tol, host_shapes=None):
+    from msda_cases import rel_err_grad_loc
     gv, gl, ga = E.msda_backward(*inputs, host_shapes=host_shapes)
     rgv, rgl, rga = _oracle_bwd(*inputs)
     assert E.rel_err(gv, rgv) < tol
-    assert E.rel_err(gl, rgl) < tol
+    assert rel_err_grad_loc(gl, rgl, inputs[3], inputs[1]) < tol  # away from cell edges
     assert E.rel_err(ga, rga) < tol
     return gv, gl, ga
 

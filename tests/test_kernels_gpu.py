@@ -337,8 +337,8 @@ def test_add_layernorm_matches_reference(shape, xd, rd):
     y = add_norm(norm, xg, rg)
     assert y.grad_fn is not None and "AddLayerNorm" in type(y.grad_fn).__name__
     y.backward(dy.to(DEV))
-    xd64 = x.double().requires_grad_(True)
-    rd64 = r.double().requires_grad_(True)
+    xd64 = x.detach().double().requires_grad_(True)
+    rd64 = r.detach().double().requires_grad_(True)
     wd = norm.weight.detach().double().cpu().requires_grad_(True)
     bd = norm.bias.detach().double().cpu().requires_grad_(True)
     ref = torch.nn.functional.layer_norm(xd64 + rd64, (c,), wd, bd, norm.eps)
