@@ -47,10 +47,22 @@ def test_bi_attention_fwd_bwd(dtype, tol, shape):
     dev_in = [x.to(DEV).requires_grad_(True) for x in (q, k, vv, vl)]
     ov, ol = bi_attention_hip(*dev_in, pad_v.to(DEV), pad_l.to(DEV), 0.0)
     ((ov.float() * gv.to(DEV, torch.float32)).sum() + (ol.float() * gl.to(DEV, torch.float32)).sum()).backward()
-    assert _rel(ov.cpu(), rv.detach()) < tol
-    assert _rel(ol.cpu(), rl.detach()) < tol
     for name, mine, ref in zip(("dq", "dk", "dvv", "dvl"), dev_in, ref_in):
         assert _rel(mine.grad.cpu(), ref.grad) < tol * 3, name
+    if dtype == torch.float32:
+        assert _rel(ov.cpu(), rv.detach()) < tol
+        assert _rel(ol.cpu(), rl.detach()) < tol
+    else:
+        # bf16: against the reference module's own statements under bf16
+        # autocast (scores and the probabilities fed to the output bmm
+        # rounded to bf16, softmax in fp32) -- what the reference computes in
+        # bf16 training; with T = 128 text tokens averaged per image token that
+        # rounding alone reaches ~1.5 % of the largest output against fp64
+        with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+            av, al = bi_attention_ref(*[x.float() for x in (q, k, vv, vl)], pad_v, pad_l)
+        assert _rel(ov.cpu(), av.double()) < tol
+        assert _rel(ol.cpu(), al.double()) < tol
+        assert _rel(ov.cpu(), rv.detach()) < 3 * tol and _rel(ol.cpu(), rl.detach()) < 3 * tol
 
 
 def test_bi_attention_production_shape_bf16():
