@@ -283,6 +283,15 @@ gd_status gd_contrastive_forward(gd_dtype dtype, const void* x, const int64_t* x
  * bytes of device memory.  Deterministic (fixed-order reduction).
  */
 int gd_wgrad_splits(int T, int O, int I);
+/* Batched form: out[b] = grad_y[b]^T x[b] for b < batch (batch strides in
+ * elements), written in out_dtype (F32 or BF16) with batch stride
+ * batch_stride_out; grad_b only for batch == 1.  Used for the
+ * image-token-long products of BiAttention (P_l^T v_v, P_v^T dO_v, dS^T q).
+ * workspace: gd_wgrad_workspace_bytes(O, I, batch * splits) bytes. */
+gd_status gd_wgrad_batched(gd_dtype dtype, const void* grad_y, int64_t ldy, int64_t batch_stride_y,
+                           const void* x, int64_t ldx, int64_t batch_stride_x, int T, int O, int I,
+                           int batch, int splits, void* workspace, gd_dtype out_dtype, void* out,
+                           int64_t batch_stride_out, float* grad_b, gd_stream_t stream);
 size_t gd_wgrad_workspace_bytes(int O, int I, int splits);
 gd_status gd_wgrad(gd_dtype dtype, const void* grad_y, int64_t ldy, const void* x, int64_t ldx, int T,
                    int O, int I, int splits, void* workspace, float* grad_w, float* grad_b,

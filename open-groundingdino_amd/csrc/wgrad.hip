@@ -23,6 +23,12 @@ namespace gd {
 namespace {
 #include "mfma_frag.inc"
 
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st4(uint16_t* p, float4 v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(uint32_t(f32_to_bf16(v.x)) | (uint32_t(f32_to_bf16(v.y)) << 16),
+                                            uint32_t(f32_to_bf16(v.z)) | (uint32_t(f32_to_bf16(v.w)) << 16));
+}
+
 template <typename T> __device__ __forceinline__ float to_float(T v);
 template <> __device__ __forceinline__ float to_float<float>(float v) { return v; }
 template <> __device__ __forceinline__ float to_float<uint16_t>(uint16_t v) { return bf16_to_f32(v); }
@@ -69,16 +75,22 @@ __device__ __forceinline__ void stage_chunk(T* xt, const T* src, int64_t ld, int
   }
 }
 
+// grid (I/64, O/64, batch * splits); batch b reads dy + b*bsy, x + b*bsx
 template <typename T>
 __global__ void __launch_bounds__(256)
-wgrad_kernel(const T* __restrict__ dy, int64_t ldy, const T* __restrict__ x, int64_t ldx, int T_, int O, int I,
-             int tokens_per_split, float* __restrict__ part_w, float* __restrict__ part_b) {
+wgrad_kernel(const T* __restrict__ dy, int64_t ldy, int64_t bsy, const T* __restrict__ x, int64_t ldx, int64_t bsx,
+             int T_, int O, int I, int splits, int tokens_per_split, float* __restrict__ part_w,
+             float* __restrict__ part_b) {
   __shared__ __attribute__((aligned(16))) T ys[64 * kWgRow];  // dY^T chunk: [o][t]
   __shared__ __attribute__((aligned(16))) T xs[64 * kWgRow];  // X^T chunk:  [i][t]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int wo = wave >> 1, wi = wave & 1;  // the wave's 32 x 32 quarter
-  const int i0 = blockIdx.x * 64, o0 = blockIdx.y * 64, split = blockIdx.z;
+  const int i0 = blockIdx.x * 64, o0 = blockIdx.y * 64;
+  const int bz = blockIdx.z / splits, split = blockIdx.z - bz * splits;
+  dy += bz * bsy;
+  x += bz * bsx;
+  const int64_t part = int64_t(bz) * splits + split;  // partial slot
   const int tb = split * tokens_per_split;
   const int te = min(T_, tb + tokens_per_split);
   const bool do_bias = part_b != nullptr && blockIdx.x == 0;
@@ -110,7 +122,7 @@ wgrad_kernel(const T* __restrict__ dy, int64_t ldy, const T* __restrict__ x, int
       for (int n = 0; n < 2; ++n) acc[m][n] = wmma(af[m], bf[n], acc[m][n]);
   }
   // partial tile: (o0 + 32wo + 16m + 4g + r, i0 + 32wi + 16n + c)
-  float* pw = part_w + int64_t(split) * O * I;
+  float* pw = part_w + part * O * I;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -120,26 +132,31 @@ wgrad_kernel(const T* __restrict__ dy, int64_t ldy, const T* __restrict__ x, int
         const int o = o0 + 32 * wo + 16 * m + 4 * g + r, i = i0 + 32 * wi + 16 * n + c;
         pw[int64_t(o) * I + i] = acc[m][n][r];
       }
-  if (do_bias && threadIdx.x < 64) part_b[int64_t(split) * O + o0 + threadIdx.x] = bsum;
+  if (do_bias && threadIdx.x < 64) part_b[part * O + o0 + threadIdx.x] = bsum;
 }
 
-// dW = sum over splits (float4 lanes), db likewise
+// out[b] = sum over splits of the partials (4 columns per thread), written in
+// fp32 or bf16 with batch stride ob; db (batch 1) likewise
+template <typename TO>
 __global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ part_b, int splits, int64_t nw4,
-                    int O, float* __restrict__ dw, float* __restrict__ db) {
+wgrad_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ part_b, int splits, int batch,
+                    int O, int I, TO* __restrict__ out, int64_t ob, float* __restrict__ db) {
   const int64_t t = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (t < nw4) {
+  const int64_t nw4 = int64_t(O) * I / 4;  // float4 groups per batch item
+  if (t < nw4 * batch) {
+    const int64_t b = t / nw4, e = t - b * nw4;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int k = 0; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(part_w)[int64_t(k) * nw4 + t];
+      const float4 v = reinterpret_cast<const float4*>(part_w)[(b * splits + k) * nw4 + e];
       s.x += v.x;
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
     }
-    reinterpret_cast<float4*>(dw)[t] = s;
-  } else if (db && t < nw4 + O) {
-    const int o = int(t - nw4);
+    TO* o = out + b * ob + e * 4;
+    st4(o, s);
+  } else if (db && t < nw4 * batch + O) {
+    const int o = int(t - nw4 * batch);
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += part_b[int64_t(k) * O + o];
     db[o] = s;
@@ -165,34 +182,53 @@ extern "C" int gd_wgrad_splits(int T, int O, int I) {
   return s < 1 ? 1 : (s > cap ? cap : s);
 }
 
+extern "C" gd_status gd_wgrad_batched(gd_dtype dt, const void* grad_y, int64_t ldy, int64_t batch_stride_y,
+                                      const void* x, int64_t ldx, int64_t batch_stride_x, int T, int O, int I,
+                                      int batch, int splits, void* workspace, gd_dtype out_dtype, void* out,
+                                      int64_t batch_stride_out, float* grad_b, gd_stream_t stream) {
+  GD_REQUIRE(dt == GD_F32 || dt == GD_BF16, "wgrad: dtype %d not supported (F32, BF16)", int(dt));
+  GD_REQUIRE(out_dtype == GD_F32 || out_dtype == GD_BF16, "wgrad: out dtype %d not supported", int(out_dtype));
+  GD_REQUIRE(T >= 0 && O > 0 && I > 0 && O % 64 == 0 && I % 64 == 0 && splits >= 1 && batch >= 1 &&
+                 int64_t(batch) * splits < 65536 && O / 64 < 65536,
+             "wgrad: bad sizes T=%d O=%d I=%d (multiples of 64) batch=%d splits=%d", T, O, I, batch, splits);
+  GD_REQUIRE(!grad_b || batch == 1, "wgrad: bias gradient only for batch 1");
+  GD_REQUIRE(grad_y && x && workspace && out, "wgrad: null pointer");
+  const int64_t align = 16 / (dt == GD_BF16 ? 2 : 4);
+  GD_REQUIRE(aligned16(grad_y) && aligned16(x) && ldy % align == 0 && ldx % align == 0 && ldy >= O && ldx >= I &&
+                 batch_stride_y % align == 0 && batch_stride_x % align == 0,
+             "wgrad: rows must be 16-byte aligned (ldy=%lld ldx=%lld)", (long long)ldy, (long long)ldx);
+  GD_REQUIRE(aligned16(out) && aligned16(workspace) && batch_stride_out % 8 == 0 &&
+                 (batch == 1 || batch_stride_out >= int64_t(O) * I),
+             "wgrad: out / workspace must be 16-byte aligned, batch_stride_out >= O*I");
+  hipStream_t s = as_hip(stream);
+  float* part_w = static_cast<float*>(workspace);
+  float* part_b = part_w + int64_t(batch) * splits * O * I;
+  const int tps = ((T + splits - 1) / splits + kWgChunk - 1) / kWgChunk * kWgChunk;
+  const dim3 grid(unsigned(I / 64), unsigned(O / 64), unsigned(batch * splits));
+  if (dt == GD_BF16)
+    hipLaunchKernelGGL((wgrad_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy, batch_stride_y,
+                       (const uint16_t*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
+                       grad_b ? part_b : nullptr);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<float>), grid, dim3(256), 0, s, (const float*)grad_y, ldy, batch_stride_y,
+                       (const float*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
+                       grad_b ? part_b : nullptr);
+  GD_LAUNCH_CHECK("wgrad");
+  const int64_t n = int64_t(O) * I / 4 * batch + (grad_b ? O : 0);
+  const dim3 rg(unsigned((n + 255) / 256));
+  if (out_dtype == GD_F32)
+    hipLaunchKernelGGL((wgrad_reduce_kernel<float>), rg, dim3(256), 0, s, part_w, part_b, splits, batch, O, I,
+                       (float*)out, batch_stride_out, grad_b);
+  else
+    hipLaunchKernelGGL((wgrad_reduce_kernel<uint16_t>), rg, dim3(256), 0, s, part_w, part_b, splits, batch, O, I,
+                       (uint16_t*)out, batch_stride_out, grad_b);
+  GD_LAUNCH_CHECK("wgrad_reduce");
+  return GD_OK;
+}
+
 extern "C" gd_status gd_wgrad(gd_dtype dt, const void* grad_y, int64_t ldy, const void* x, int64_t ldx, int T,
                               int O, int I, int splits, void* workspace, float* grad_w, float* grad_b,
                               gd_stream_t stream) {
-  GD_REQUIRE(dt == GD_F32 || dt == GD_BF16, "wgrad: dtype %d not supported (F32, BF16)", int(dt));
-  GD_REQUIRE(T >= 0 && O > 0 && I > 0 && O % 64 == 0 && I % 64 == 0 && splits >= 1 && splits < 65536 &&
-                 O / 64 < 65536,
-             "wgrad: bad sizes T=%d O=%d I=%d (multiples of 64) splits=%d", T, O, I, splits);
-  GD_REQUIRE(grad_y && x && workspace && grad_w, "wgrad: null pointer");
-  const int64_t align = 16 / (dt == GD_BF16 ? 2 : 4);
-  GD_REQUIRE(aligned16(grad_y) && aligned16(x) && ldy % align == 0 && ldx % align == 0 && ldy >= O && ldx >= I,
-             "wgrad: rows must be 16-byte aligned (ldy=%lld ldx=%lld)", (long long)ldy, (long long)ldx);
-  GD_REQUIRE(aligned16(grad_w) && aligned16(workspace), "wgrad: grad_w / workspace must be 16-byte aligned");
-  hipStream_t s = as_hip(stream);
-  float* part_w = static_cast<float*>(workspace);
-  float* part_b = part_w + int64_t(splits) * O * I;
-  const int tps = ((T + splits - 1) / splits + kWgChunk - 1) / kWgChunk * kWgChunk;
-  const dim3 grid(unsigned(I / 64), unsigned(O / 64), unsigned(splits));
-  if (dt == GD_BF16)
-    hipLaunchKernelGGL((wgrad_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy,
-                       (const uint16_t*)x, ldx, T, O, I, tps, part_w, grad_b ? part_b : nullptr);
-  else
-    hipLaunchKernelGGL((wgrad_kernel<float>), grid, dim3(256), 0, s, (const float*)grad_y, ldy, (const float*)x,
-                       ldx, T, O, I, tps, part_w, grad_b ? part_b : nullptr);
-  GD_LAUNCH_CHECK("wgrad");
-  const int64_t nw4 = int64_t(O) * I / 4;
-  const int64_t n = nw4 + (grad_b ? O : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, part_w, part_b, splits,
-                     nw4, O, grad_w, grad_b);
-  GD_LAUNCH_CHECK("wgrad_reduce");
-  return GD_OK;
+  return gd_wgrad_batched(dt, grad_y, ldy, 0, x, ldx, 0, T, O, I, 1, splits, workspace, GD_F32, grad_w,
+                          int64_t(O) * I, grad_b, stream);
 }

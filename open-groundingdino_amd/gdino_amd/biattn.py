@@ -20,7 +20,7 @@ import ctypes
 
 import torch
 
-from . import _lib, kernels
+from . import _lib, kernels, wgrad
 
 _p, _i = ctypes.c_void_p, ctypes.c_int
 _lib.register("gd_biattn_softmax_fwd", [_i, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
@@ -71,12 +71,67 @@ class BiSoftmax(torch.autograd.Function):
         return ds, None, None
 
 
+class _QKt(torch.autograd.Function):
+    """s = q k^T; dk = dS^T q is the long-K (S image tokens) product."""
+
+    @staticmethod
+    def forward(ctx, q, k):
+        ctx.save_for_backward(q, k)
+        return torch.matmul(q, k.transpose(-1, -2))
+
+    @staticmethod
+    def backward(ctx, ds):
+        q, k = ctx.saved_tensors
+        ds = ds.to(q.dtype).contiguous()
+        return torch.matmul(ds, k), wgrad.tn_matmul(ds, q.contiguous())
+
+
+class _PV(torch.autograd.Function):
+    """out_v = P_v v_l; dv_l = P_v^T dout_v is the long-K product."""
+
+    @staticmethod
+    def forward(ctx, pv, vl):
+        ctx.save_for_backward(pv, vl)
+        return torch.matmul(pv, vl)
+
+    @staticmethod
+    def backward(ctx, dout):
+        pv, vl = ctx.saved_tensors
+        dout = dout.to(pv.dtype).contiguous()
+        return torch.matmul(dout, vl.transpose(-1, -2)), wgrad.tn_matmul(pv, dout)
+
+
+class _PlTV(torch.autograd.Function):
+    """out_l = P_l^T v_v (long-K forward); its gradients are ordinary GEMMs."""
+
+    @staticmethod
+    def forward(ctx, pl, vv):
+        ctx.save_for_backward(pl, vv)
+        return wgrad.tn_matmul(pl, vv.contiguous())
+
+    @staticmethod
+    def backward(ctx, dout):
+        pl, vv = ctx.saved_tensors
+        dout = dout.to(pl.dtype)
+        return torch.matmul(vv, dout.transpose(-1, -2)), torch.matmul(pl, dout)
+
+
+def _long_k_ok(q, k, v_v, v_l):
+    """the three S-long products on the split-K kernel (gdino_amd/wgrad.py)"""
+    return (q.dtype == k.dtype == v_v.dtype == v_l.dtype and wgrad.tn_eligible(q, q)
+            and k.shape[-2] % 64 == 0 and q.shape[-1] % 64 == 0)
+
+
 def bi_attention_hip(q, k, v_v, v_l, pad_v=None, pad_l=None, dropout_p=0.0):
     """Same contract as kernels._bi_attention_torch (q pre-scaled)."""
     if dropout_p > 0.0:
         # attention-probability dropout (fusion_dropout > 0) is not fused;
         # the SDPA composition implements it.
         return kernels._bi_attention_torch(q, k, v_v, v_l, pad_v, pad_l, dropout_p)
+    if _long_k_ok(q, k, v_v, v_l):
+        s = _QKt.apply(q, k)
+        pv, pl = BiSoftmax.apply(s, pad_v, pad_l)
+        return _PV.apply(pv, v_l), _PlTV.apply(pl, v_v)
     s = torch.matmul(q, k.transpose(-1, -2))
     pv, pl = BiSoftmax.apply(s, pad_v, pad_l)
     out_v = torch.matmul(pv.to(v_l.dtype) if pv.dtype != v_l.dtype else pv, v_l)

@@ -26,6 +26,8 @@ from . import _lib
 _p, _i, _i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 _lib.register("gd_wgrad", [_i, _p, _i64, _p, _i64, _i, _i, _i, _i, _p, _p, _p, _p])
 _lib.register("gd_wgrad_splits", [_i, _i, _i])  # returns int (the registered restype)
+_lib.register("gd_wgrad_batched", [_i, _p, _i64, _i64, _p, _i64, _i64, _i, _i, _i, _i, _i, _p, _i, _p, _i64, _p,
+                                   _p])
 
 MIN_TOKENS = 4096
 MAX_TILES = 32  # O/64 * I/64: beyond this the library GEMM has enough output tiles
@@ -63,6 +65,32 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, want_bias: bool):
     _lib.call("gd_wgrad", _lib.dtype_code(dy2), dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), t, o, i,
               s, ws.data_ptr(), dw.data_ptr(), _lib.ptr(db), _lib.stream_of(dy2))
     return dw, db
+
+
+def tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """a^T b over the token dimension (-2) with the split-K kernel?"""
+    return (_lib.enabled("wgrad") and _lib.on_device(a) and a.dtype == b.dtype
+            and a.dtype in (torch.float32, torch.bfloat16) and a.shape[:-1] == b.shape[:-1]
+            and a.shape[-2] >= MIN_TOKENS and a.shape[-1] % 64 == 0 and b.shape[-1] % 64 == 0)
+
+
+def tn_matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [..., T, O], b [..., T, I] -> a^T b [..., O, I] in a's dtype (fp32
+    accumulation), batched over the leading dims: the long-K products whose
+    K (= T tokens) dwarfs the O x I output."""
+    t, o, i = a.shape[-2], a.shape[-1], b.shape[-1]
+    lead = a.shape[:-2]
+    a2 = a.reshape(-1, t, o).contiguous()
+    b2 = b.reshape(-1, t, i).contiguous()
+    nb = a2.shape[0]
+    tiles = (o // 64) * (i // 64)
+    s = max(1, min(max(t // 256, 1), -(-1024 // (tiles * nb))))
+    ws = _workspace(o, i, s * nb, a.device)
+    out = torch.empty(nb, o, i, dtype=a.dtype, device=a.device)
+    _lib.call("gd_wgrad_batched", _lib.dtype_code(a2), a2.data_ptr(), a2.stride(1), a2.stride(0), b2.data_ptr(),
+              b2.stride(1), b2.stride(0), t, o, i, nb, s, ws.data_ptr(), _lib.dtype_code(out), out.data_ptr(),
+              out.stride(0), None, _lib.stream_of(a2))
+    return out.reshape(*lead, o, i)
 
 
 class TokenLinear(torch.autograd.Function):

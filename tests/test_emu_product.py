@@ -117,3 +117,45 @@ def test_token_linear_emulated_matches_library_linear():
     for k, ref in ((1, wd.grad), (2, bd.grad), (3, xd.grad)):
         assert _rel(res[True][k], ref) < 1e-2
         assert _rel(res[True][k], ref) <= _rel(res[False][k], ref) * 1.5 + 1e-6, k
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+def test_tn_matmul_batched(dtype, tol):
+    """a^T b over 300 tokens, batched over [2, 3], bf16 / fp32 output."""
+    from gdino_amd.wgrad import tn_matmul
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(2, 3, 300, 128, generator=g).to(dtype)
+    b = torch.randn(2, 3, 300, 64, generator=g).to(dtype)
+    with emu_product.emulated_product(min_tokens=64):
+        out = tn_matmul(a, b)
+    assert out.shape == (2, 3, 128, 64) and out.dtype == dtype
+    assert _rel(out.float(), a.double().transpose(-1, -2) @ b.double()) < tol
+
+
+def test_bi_attention_long_k_products_on_the_split_k_kernel():
+    """BiAttention with its three image-token-long products (out_l = P_l^T v_v,
+    dv_l = P_v^T dout_v, dk = dS^T q) on the split-K kernel, fp32, against the
+    reference restatement with gradients."""
+    from gdino_amd import biattn
+    from oracle.blocks import bi_attention_ref
+    g = torch.Generator().manual_seed(1)
+    b, h, s, t, hd = 1, 2, 300, 64, 64
+    q = torch.randn(b, h, s, hd, generator=g) * hd ** -0.5
+    k, vl = torch.randn(b, h, t, hd, generator=g), torch.randn(b, h, t, hd, generator=g)
+    vv = torch.randn(b, h, s, hd, generator=g)
+    pad_v = torch.zeros(b, s, dtype=torch.bool)
+    pad_v[0, 250:] = True
+    pad_l = torch.zeros(b, t, dtype=torch.bool)
+    pad_l[0, 40:] = True
+    gv, gl = torch.randn(b, h, s, hd, generator=g), torch.randn(b, h, t, hd, generator=g)
+    mine = [x.clone().requires_grad_(True) for x in (q, k, vv, vl)]
+    with emu_product.emulated_product(min_tokens=64):
+        assert biattn._long_k_ok(*mine[:2], *mine[2:])
+        ov, ol = biattn.bi_attention_hip(*mine, pad_v, pad_l)
+        ((ov * gv).sum() + (ol * gl).sum()).backward()
+    ref = [x.double().requires_grad_(True) for x in (q, k, vv, vl)]
+    rv, rl = bi_attention_ref(*ref, pad_v, pad_l)
+    ((rv * gv.double()).sum() + (rl * gl.double()).sum()).backward()
+    assert _rel(ov, rv) < 1e-5 and _rel(ol, rl) < 1e-5
+    for a, r in zip(mine, ref):
+        assert _rel(a.grad, r.grad) < 1e-5

@@ -360,3 +360,16 @@ def test_add_layernorm_matches_reference(shape, xd, rd):
     assert _rel(rg.grad.cpu(), rd64.grad) < (1e-2 if rd == torch.bfloat16 else 1e-5)
     assert _rel(norm.weight.grad.cpu(), wd.grad) < 1e-5
     assert _rel(norm.bias.grad.cpu(), bd.grad) < 1e-5
+
+
+def test_tn_matmul_biattention_shape():
+    """out_l = P_l^T v_v of the fusion layer at 800x1333 bs=2: 8 (b, h) pairs,
+    22 223 image tokens, 256 text tokens x head_dim 256, bf16 in / out."""
+    from gdino_amd.wgrad import tn_matmul
+    g = torch.Generator().manual_seed(0)
+    a = torch.rand(2, 4, 22223, 256, generator=g).to(torch.bfloat16)
+    b = torch.randn(2, 4, 22223, 256, generator=g).to(torch.bfloat16)
+    out = tn_matmul(a.to(DEV), b.to(DEV))
+    torch.cuda.synchronize()
+    assert out.dtype == torch.bfloat16
+    assert _rel(out.cpu(), a.double().transpose(-1, -2) @ b.double()) < 1e-2
