@@ -94,7 +94,13 @@ extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, 
   a.lse = lse;
   hipStream_t s = as_hip(stream);
   const dim3 grid(unsigned((Lq + 255) / 256), unsigned(B * H));
-#define GD_AF(T, HD) hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(256), 0, s, a)
+#define GD_AF(T, HD)                                                                         \
+  do {                                                                                       \
+    if (a.dropout)                                                                           \
+      hipLaunchKernelGGL((attn_fwd_kernel<T, HD, true>), grid, dim3(256), 0, s, a);          \
+    else                                                                                     \
+      hipLaunchKernelGGL((attn_fwd_kernel<T, HD, false>), grid, dim3(256), 0, s, a);         \
+  } while (0)
   if (dt == GD_BF16) {
     if (head_dim == 32) GD_AF(uint16_t, 32); else GD_AF(uint16_t, 64);
   } else {
@@ -137,9 +143,15 @@ extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk,
   const dim3 gk(unsigned((Lk + 127) / 128), unsigned(B * H));
 #define GD_AB(T, HD)                                                                  \
   do {                                                                                \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD>), gq, dim3(256), 0, s, a);          \
-    GD_LAUNCH_CHECK("attn_bwd_dq");                                                   \
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD>), gk, dim3(256), 0, s, a);         \
+    if (a.dropout) {                                                                  \
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD, true>), gq, dim3(256), 0, s, a);  \
+      GD_LAUNCH_CHECK("attn_bwd_dq");                                                 \
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD, true>), gk, dim3(256), 0, s, a); \
+    } else {                                                                          \
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD, false>), gq, dim3(256), 0, s, a); \
+      GD_LAUNCH_CHECK("attn_bwd_dq");                                                 \
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD, false>), gk, dim3(256), 0, s, a);\
+    }                                                                                 \
     GD_LAUNCH_CHECK("attn_bwd_dkv");                                                  \
   } while (0)
   if (dt == GD_BF16) {
