@@ -318,9 +318,9 @@ def test_token_linear_matches_autocast_linear():
         (y.float() * gy).sum().backward()
         res[flag] = (y.float(), lin.weight.grad.clone(), lin.bias.grad.clone(), xi.grad.clone())
     wgrad.ENABLED = True
-    xd = x.double().requires_grad_(True)
-    wd = lin.weight.double().requires_grad_(True)
-    bd = lin.bias.double().requires_grad_(True)
+    xd = x.detach().double().requires_grad_(True)
+    wd = lin.weight.detach().double().requires_grad_(True)
+    bd = lin.bias.detach().double().requires_grad_(True)
     yd = torch.nn.functional.linear(xd, wd, bd)
     (yd * gy.double()).sum().backward()
     torch.testing.assert_close(res[True][0], res[False][0], rtol=0, atol=0)
