@@ -213,29 +213,39 @@ def test_emulated_kernels_under_other_schedules(sched):
 
 
 # ------------------------------------------------------ AddressSanitizer
-_ASAN_SCRIPT = r"""
+_ASAN_HEAD = r"""
 import sys
 sys.path[:0] = {paths!r}
 import torch
 import test_emu_kernels as t
 S = sum(h * w for h, w in t.MEDIUM)
+"""
+# three groups, run as concurrent processes (the ASan build is ~10x slower)
+_ASAN_GROUPS = [
+    r"""
 t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=3, local=True, outlier_frac=0.1), 1e-5)
-t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)
 t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 37, seed=6), 1e-5)
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=8, local=True, outlier_frac=0.02), 1e-5,
              host_shapes=t.WIDE)
+""",
+    r"""
+t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 2, 200, 100))
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
+t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
+t.test_emulated_msda_prologue(2, torch.bfloat16)
+t.test_emulated_msda_prologue(4, torch.float32)
+""",
+    r"""
 t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)
 t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
 t.test_emulated_attention(2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh")
 t.test_emulated_attention(1, 1, 33, 300, 32, "add", torch.float32, 1e-5, "blh")
-t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
-t.test_emulated_msda_prologue(2, torch.bfloat16)
-t.test_emulated_msda_prologue(4, torch.float32)
 t.test_emulated_attention_dropout(torch.float32, 1e-5)
-print("asan-clean")
-"""
+t.test_emulated_wgrad(777, 64, 192, 3, torch.float32, 1e-6)
+t.test_emulated_add_layernorm(50, 192, torch.float32, torch.float32)
+""",
+]
 
 
 def test_emulated_kernels_under_address_sanitizer():
@@ -249,10 +259,14 @@ def test_emulated_kernels_under_address_sanitizer():
     if not os.path.exists(rt):
         pytest.skip("clang ASan runtime not available")
     paths = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "open-groundingdino_amd")]
-    env = dict(os.environ, GD_EMU_ASAN="1", LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0")
-    r = subprocess.run([sys.executable, "-c", _ASAN_SCRIPT.format(paths=paths)], env=env, capture_output=True,
-                       text=True, timeout=900)
-    assert r.returncode == 0 and "asan-clean" in r.stdout, r.stderr[-4000:]
+    env = dict(os.environ, GD_EMU_ASAN="1", LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0", OMP_NUM_THREADS="1")
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "emu"), "asan"], check=True)
+    procs = [subprocess.Popen([sys.executable, "-c", _ASAN_HEAD.format(paths=paths) + g + 'print("asan-clean")'],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for g in _ASAN_GROUPS]
+    for p in procs:
+        out, err = p.communicate(timeout=900)
+        assert p.returncode == 0 and "asan-clean" in out, err[-4000:]
 
 
 # ------------------------------------------- Swin window attention (MFMA)
