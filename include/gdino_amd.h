@@ -38,6 +38,11 @@
  *                        and its autograd backward incl. the scatter into
  *                        relative_position_bias_table
  *                        models/GroundingDINO/backbone/swin_transformer.py:134-174
+ *   gd_window_attn_image_forward / _backward
+ *                     <- the same plus SwinTransformerBlock.forward's zero
+ *                        pad, cyclic shift, window partition, window reverse,
+ *                        roll back and crop
+ *                        models/GroundingDINO/backbone/swin_transformer.py:238-292
  *
  *   gd_attn_forward / _backward
  *                     <- the attention cores the reference runs as eager
@@ -219,6 +224,29 @@ gd_status gd_window_attn_backward(gd_dtype dtype, const void* qkv, const float* 
                                   const void* grad_out, const float* lse, int B_, int N, int nH,
                                   int head_dim, int nW, float scale, void* grad_qkv,
                                   float* grad_table, gd_stream_t stream);
+/*
+ * The same on the UNPARTITIONED image: qkv [B, H*W, 3, nH, head_dim] (the qkv
+ * Linear of the normed tokens, row-major over (y, x)) -> out [B, H*W, nH*head_dim].
+ * The image is zero-padded to Hp x Wp (multiples of `window`), rolled by
+ * -shift and cut into B * (Hp/window) * (Wp/window) windows of N = window^2
+ * tokens, exactly as the reference; a pad position's q/k/v is qkv_bias
+ * [3, nH, head_dim] (same dtype as qkv; the Linear of a zero row), or zeros
+ * when qkv_bias is NULL.  mask (NULL when shift == 0) is [nW_image, N, N].
+ * lse is [B * nW_image, nH, N].
+ */
+gd_status gd_window_attn_image_forward(gd_dtype dtype, const void* qkv, const void* qkv_bias,
+                                       const float* table, const int64_t* rel_index, const float* mask,
+                                       int B, int H, int W, int window, int shift, int nH, int head_dim,
+                                       float scale, void* out, float* lse, gd_stream_t stream);
+/* grad_qkv [B, H*W, 3, nH, head_dim] is written; grad_qkv_bias [3, nH,
+ * head_dim] F32 (the pad positions' share of the qkv bias gradient; ignored
+ * when qkv_bias is NULL) and grad_table are ACCUMULATED into. */
+gd_status gd_window_attn_image_backward(gd_dtype dtype, const void* qkv, const void* qkv_bias,
+                                        const float* table, const int64_t* rel_index, const float* mask,
+                                        const void* out, const void* grad_out, const float* lse, int B,
+                                        int H, int W, int window, int shift, int nH, int head_dim,
+                                        float scale, void* grad_qkv, float* grad_qkv_bias,
+                                        float* grad_table, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Masked multi-head attention (flash-style; scores never reach HBM)         */

@@ -6,6 +6,9 @@ primitives, so that the implementation behind each op is one swap:
   window_attention   Swin W-MSA / SW-MSA core   swin_transformer.py:134-174
   window_attention_packed  the same on the packed qkv Linear output with the
                      bias table + index (what WindowAttention.forward calls)
+  window_attention_image  the same on the unpartitioned image's qkv, with the
+                     Swin block's pad / roll / partition / reverse / crop
+                     (swin_transformer.py:250-290) fused in
   attention          masked attention (BERT self-attn, text enhancer, decoder
                      self-attn and text cross-attn): gdino_amd/attn.py
   bi_attention       BiMultiHeadAttention core   fuse_modules.py:162-246
@@ -126,6 +129,13 @@ def window_attention_packed(qkv, table, rel_index, mask, scale):
     """qkv [B_, N, 3, nH, hd], table [(2Wh-1)(2Ww-1), nH], rel_index [N*N],
     mask [nW, N, N] or None -> [B_, N, nH*hd] (gdino_amd/wattn.py)."""
     return get("window_attention_packed")(qkv, table, rel_index, mask, scale)
+
+
+def window_attention_image(qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale):
+    """qkv [B, H*W, 3C] (the qkv Linear of the normed tokens), qkv_bias [3C]
+    or None, mask [nW, N, N] (used when shift > 0) -> [B, H*W, C]
+    (gdino_amd/wattn.py)."""
+    return get("window_attention_image")(qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale)
 
 
 def attention(q, k, v, attn_mask=None, scale=None, dropout_p=0.0):

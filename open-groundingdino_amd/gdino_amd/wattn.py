@@ -17,6 +17,15 @@ Contract of ``window_attention_packed(qkv, table, rel_index, mask, scale)``:
                                   consecutive (window b uses mask[b % nW])
   -> [B_, N, nH*hd]               the layout the proj Linear reads
 
+``window_attention_image(qkv, qkv_bias, table, rel_index, mask, hw, ws,
+shift, scale)`` is the same on the qkv Linear output of the unpartitioned
+image [B, H*W, 3C] -> [B, H*W, C]: SwinTransformerBlock.forward's zero pad,
+cyclic shift, window partition, window reverse, roll back and crop
+(swin_transformer.py:250-290) are the kernel's row map, so none of those
+copies (nor their backward) is launched.  A pad position's q/k/v is the qkv
+bias (the Linear of the zero pad row); its gradient is returned as the bias
+gradient, which autograd adds to the Linear's own.
+
 The HIP kernel covers N <= 64 (window <= 8) and hd = 32 (every Swin-T/S/B/L
 head) in fp32 and bf16.  Other shapes (Swin-B/384's 12x12 windows, N = 144)
 and dtypes use the torch composition (ROCm library kernels); CPU tensors
@@ -33,6 +42,8 @@ from . import _lib, kernels
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register("gd_window_attn_forward", [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _p, _p, _p])
 _lib.register("gd_window_attn_backward", [_i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _p, _p, _p])
+_lib.register("gd_window_attn_image_forward", [_i] + [_p] * 5 + [_i] * 7 + [_f, _p, _p, _p])
+_lib.register("gd_window_attn_image_backward", [_i] + [_p] * 8 + [_i] * 7 + [_f, _p, _p, _p, _p])
 
 MAX_TOKENS = 64
 
@@ -92,5 +103,90 @@ def window_attention_packed_torch(qkv, table, rel_index, mask, scale):
     return out.transpose(1, 2).reshape(b_, n, nh * hd)
 
 
+class WindowAttnImageFunction(torch.autograd.Function):
+    """gd_window_attn_image_*: the window attention of one SwinTransformerBlock
+    on the qkv Linear output of the unpartitioned image; the block's pad,
+    roll, partition, reverse, roll back and crop are the kernel's row map."""
+
+    @staticmethod
+    def forward(ctx, qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale):
+        _lib.require_device(qkv, qkv_bias, table, rel_index, mask, what="window_attention_image")
+        qkv = qkv.contiguous()
+        bias = None if qkv_bias is None else qkv_bias.detach().to(qkv.dtype).contiguous()
+        table32 = table.detach().float().contiguous()
+        ridx = rel_index.to(torch.int64).contiguous()
+        mask32 = None if (mask is None or shift == 0) else mask.float().contiguous()
+        b, _, c3 = qkv.shape
+        nh = table.shape[1]
+        hd = c3 // (3 * nh)
+        hp, wp = -(-hw[0] // ws) * ws, -(-hw[1] // ws) * ws
+        out = torch.empty(b, hw[0] * hw[1], c3 // 3, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(b * (hp // ws) * (wp // ws), nh, ws * ws, dtype=torch.float32, device=qkv.device)
+        _lib.call("gd_window_attn_image_forward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
+                  table32.data_ptr(), ridx.data_ptr(), _lib.ptr(mask32), b, hw[0], hw[1], ws, shift, nh, hd,
+                  float(scale), out.data_ptr(), lse.data_ptr(), _lib.stream_of(qkv))
+        ctx.save_for_backward(qkv, bias, table32, ridx, mask32, out, lse)
+        ctx.geo = (hw, ws, shift, float(scale))
+        ctx.dtypes = (None if qkv_bias is None else qkv_bias.dtype, table.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, bias, table32, ridx, mask32, out, lse = ctx.saved_tensors
+        hw, ws, shift, scale = ctx.geo
+        b, _, c3 = qkv.shape
+        nh = table32.shape[1]
+        dout = dout.to(qkv.dtype).contiguous()
+        dqkv = torch.empty_like(qkv)
+        dbias = None if bias is None else torch.zeros(c3, dtype=torch.float32, device=qkv.device)
+        dtable = torch.zeros_like(table32)
+        _lib.call("gd_window_attn_image_backward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
+                  table32.data_ptr(), ridx.data_ptr(), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(),
+                  lse.data_ptr(), b, hw[0], hw[1], ws, shift, nh, c3 // (3 * nh), scale, dqkv.data_ptr(),
+                  _lib.ptr(dbias), dtable.data_ptr(), _lib.stream_of(qkv))
+        bias_dt, table_dt = ctx.dtypes
+        return (dqkv, None if dbias is None else dbias.to(bias_dt), dtable.to(table_dt),
+                None, None, None, None, None, None)
+
+
+def image_supported(qkv, table, ws):
+    return (_lib.enabled("wattn") and qkv.dtype in (torch.float32, torch.bfloat16) and ws * ws <= MAX_TOKENS
+            and qkv.shape[-1] == 3 * 32 * table.shape[1])
+
+
+def window_attention_image_hip(qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale):
+    if not image_supported(qkv, table, ws):
+        return window_attention_image_torch(qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale)
+    return WindowAttnImageFunction.apply(qkv, qkv_bias, table, rel_index, mask, tuple(hw), ws, shift, scale)
+
+
+def window_attention_image_torch(qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale):
+    """The same op composed from ROCm library kernels: pad (the qkv of a zero
+    row is the Linear bias), roll, partition, window attention, reverse, roll
+    back, crop."""
+    b, _, c3 = qkv.shape
+    h, w = hw
+    nh = table.shape[1]
+    hp, wp = -(-h // ws) * ws, -(-w // ws) * ws
+    x = qkv.view(b, h, w, c3)
+    if hp != h or wp != w:
+        fill = qkv.new_zeros(()) if qkv_bias is None else qkv_bias.to(qkv.dtype)
+        pad = fill.expand(b, hp, wp, c3)
+        x = torch.cat([torch.cat([x, pad[:, :h, w:]], 2), pad[:, h:]], 1)
+    if shift > 0:
+        x = torch.roll(x, shifts=(-shift, -shift), dims=(1, 2))
+    win = x.view(b, hp // ws, ws, wp // ws, ws, c3).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, 3, nh,
+                                                                                     c3 // (3 * nh))
+    out = kernels.window_attention_packed(win, table, rel_index, mask if shift > 0 else None, scale)
+    x = out.view(b, hp // ws, wp // ws, ws, ws, -1).permute(0, 1, 3, 2, 4, 5).reshape(b, hp, wp, -1)
+    if shift > 0:
+        x = torch.roll(x, shifts=(shift, shift), dims=(1, 2))
+    if hp != h or wp != w:
+        x = x[:, :h, :w]
+    return x.reshape(b, h * w, -1)
+
+
 kernels.register("window_attention_packed", "torch", window_attention_packed_torch)
 kernels.register("window_attention_packed", "hip", window_attention_packed_hip, default=True)
+kernels.register("window_attention_image", "torch", window_attention_image_torch)
+kernels.register("window_attention_image", "hip", window_attention_image_hip, default=True)

@@ -134,6 +134,26 @@ class SwinTransformerBlock(nn.Module):
         ws, sh = self.window_size, self.shift_size
         shortcut = x
         x = self.norm1(x)
+        attn = self.attn
+        if attn.attn_drop.p > 0.0 and self.training:
+            x = self._windowed_attention(x, mask_matrix)
+        else:
+            # the qkv Linear is per token, so it runs on the unpartitioned
+            # image; pad, roll, partition, the attention, reverse, roll back
+            # and crop are one kernel per direction (gdino_amd/wattn.py)
+            qkv = attn.qkv(x)
+            x = kernels.window_attention_image(qkv, attn.qkv.bias, attn.relative_position_bias_table,
+                                               attn.relative_position_index.view(-1), mask_matrix, (h, w), ws, sh,
+                                               attn.scale)
+            x = attn.proj_drop(attn.proj(x))
+        x = shortcut + self.drop_path(x)
+        return x + self.drop_path(self.mlp(self.norm2(x)))
+
+    def _windowed_attention(self, x, mask_matrix):
+        """reference :250-290 step by step (the path with attention dropout)"""
+        b, _, c = x.shape
+        h, w = self.H, self.W
+        ws, sh = self.window_size, self.shift_size
         dt = castcache.autocast_dtype(x)
         if dt is not None:
             # the qkv GEMM casts its input anyway: cast before the pad / roll /
@@ -154,8 +174,7 @@ class SwinTransformerBlock(nn.Module):
             x = torch.roll(x, shifts=(sh, sh), dims=(1, 2))
         if pad_r or pad_b:
             x = x[:, :h, :w, :]
-        x = shortcut + self.drop_path(x.reshape(b, h * w, c))
-        return x + self.drop_path(self.mlp(self.norm2(x)))
+        return x.reshape(b, h * w, c)
 
 
 class PatchMerging(nn.Module):

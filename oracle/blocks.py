@@ -10,6 +10,8 @@ reference module imports here (tests/golden/make_block_golden.py).
                        clamps, column-max shift, -inf masks, two softmaxes)
   window_attention_ref swin_transformer.py:134-174
   window_attention_packed_ref  the same on the packed qkv + bias table (:113-114, :171)
+  window_attention_image_ref   + SwinTransformerBlock's pad / roll / partition
+                               and reverse / roll back / crop (:238-292)
   attention_ref        masked softmax(q k^T * scale) v (additive / bool mask)
   contrastive_ref      utils.py:242-273
   phrase_masks_ref     bertwarper.py:224-273 (per-special-token loop)
@@ -68,6 +70,32 @@ def window_attention_packed_ref(qkv, table, rel_index, mask, scale):
     bias = table[rel_index.view(-1)].view(n, n, -1).permute(2, 0, 1).contiguous()
     out = window_attention_ref(q, k, v, bias, mask, scale)
     return out.transpose(1, 2).reshape(b_, n, nh * hd)
+
+
+def window_attention_image_ref(qkv, qkv_bias, table, rel_index, mask, hw, ws, shift, scale):
+    """SwinTransformerBlock.forward between its qkv and proj Linears
+    (swin_transformer.py:250-290 around :134-174), restated on the qkv Linear
+    output of the unpartitioned image qkv [B, H*W, 3C] -> [B, H*W, C]: the
+    normed tokens are zero-padded to multiples of ws (:255-257; a pad row's
+    qkv is the Linear bias), rolled by -shift (:262), partitioned (:269),
+    attended, reversed (:281), rolled back (:285) and cropped (:290)."""
+    b, _, c3 = qkv.shape
+    h, w = hw
+    nh = table.shape[1]
+    hp, wp = -(-h // ws) * ws, -(-w // ws) * ws
+    x = qkv.new_zeros(b, hp, wp, c3)
+    if qkv_bias is not None:
+        x = x + qkv_bias.to(qkv.dtype)
+    x = torch.cat([torch.cat([qkv.view(b, h, w, c3), x[:, :h, w:]], 2), x[:, h:]], 1)
+    if shift > 0:
+        x = torch.roll(x, shifts=(-shift, -shift), dims=(1, 2))
+    win = x.view(b, hp // ws, ws, wp // ws, ws, c3).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws * ws, 3, nh,
+                                                                                     c3 // (3 * nh))
+    out = window_attention_packed_ref(win, table, rel_index, mask if shift > 0 else None, scale)
+    x = out.view(b, hp // ws, wp // ws, ws, ws, -1).permute(0, 1, 3, 2, 4, 5).reshape(b, hp, wp, -1)
+    if shift > 0:
+        x = torch.roll(x, shifts=(shift, shift), dims=(1, 2))
+    return x[:, :h, :w].reshape(b, h * w, -1)
 
 
 def attention_ref(q, k, v, mask=None, scale=None):

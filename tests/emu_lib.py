@@ -38,6 +38,8 @@ def lib():
         _LIB.gd_window_attn_backward.argtypes = ([_i, _p, _p, _p, _p, _p, _p, _p] + [_i] * 5 +
                                                  [ctypes.c_float, _p, _p, _p])
         _f, _u = ctypes.c_float, ctypes.c_uint32
+        _LIB.gd_window_attn_image_forward.argtypes = [_i] + [_p] * 5 + [_i] * 7 + [_f, _p, _p, _p]
+        _LIB.gd_window_attn_image_backward.argtypes = [_i] + [_p] * 8 + [_i] * 7 + [_f, _p, _p, _p, _p]
         _LIB.gd_attn_forward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u, _p, _p, _p, _p]
         _LIB.gd_attn_backward.argtypes = [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u] + [_p] * 13
         _LIB.gd_contrastive_forward.argtypes = [_i] + [_p] * 5 + [_i] * 5 + [_p, _p, _p]
@@ -156,6 +158,43 @@ def window_attn_backward(qkv, table, ridx, mask, scale, out, lse, grad_out):
                                          _ptr(grad_out), _ptr(lse), B_, N, nH, hd, nW, scale, _ptr(gq), _ptr(gt),
                                          None))
     return gq, gt
+
+
+def window_attn_image_forward(qkv, qkv_bias, table, ridx, mask, hw, ws, shift, scale):
+    """qkv [B, H*W, 3C] (f32/bf16), qkv_bias [3C] or None -> out [B, H*W, C],
+    lse [B*nW, nH, ws*ws] (gd_window_attn_image_forward)."""
+    b, _, c3 = qkv.shape
+    nh = table.shape[1]
+    hd = c3 // (3 * nh)
+    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    bias = None if qkv_bias is None else qkv_bias.to(qkv.dtype).contiguous()
+    mask = None if mask is None else mask.float().contiguous()
+    hp, wp = -(-hw[0] // ws) * ws, -(-hw[1] // ws) * ws
+    out = torch.full((b, hw[0] * hw[1], c3 // 3), float("nan"), dtype=qkv.dtype)
+    lse = torch.empty(b * (hp // ws) * (wp // ws), nh, ws * ws, dtype=torch.float32)
+    _check(lib().gd_window_attn_image_forward(_code(qkv), _ptr(qkv), _ptr(bias), _ptr(table), _ptr(ridx),
+                                              _ptr(mask), b, hw[0], hw[1], ws, shift, nh, hd, scale, _ptr(out),
+                                              _ptr(lse), None))
+    return out, lse
+
+
+def window_attn_image_backward(qkv, qkv_bias, table, ridx, mask, hw, ws, shift, scale, out, lse, grad_out):
+    """-> grad_qkv (qkv dtype), grad_qkv_bias (f32 [3C], pad rows only; None
+    without a bias), grad_table (f32)."""
+    b, _, c3 = qkv.shape
+    nh = table.shape[1]
+    hd = c3 // (3 * nh)
+    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    bias = None if qkv_bias is None else qkv_bias.to(qkv.dtype).contiguous()
+    mask = None if mask is None else mask.float().contiguous()
+    gq = torch.full_like(qkv, float("nan"))
+    gb = None if bias is None else torch.zeros(c3, dtype=torch.float32)
+    gt = torch.zeros_like(table)
+    _check(lib().gd_window_attn_image_backward(_code(qkv), _ptr(qkv), _ptr(bias), _ptr(table), _ptr(ridx),
+                                               _ptr(mask), _ptr(out.contiguous()), _ptr(grad_out.contiguous()),
+                                               _ptr(lse), b, hw[0], hw[1], ws, shift, nh, hd, scale, _ptr(gq),
+                                               _ptr(gb), _ptr(gt), None))
+    return gq, gb, gt
 
 
 def _st3(t):

@@ -17,7 +17,8 @@ def oracle_msda():
     """Route every HIP-only op to its oracle restatement (CPU tests)."""
     import models.GroundingDINO.ms_deform_attn as mod
     from gdino_amd import kernels
-    from oracle.blocks import attention_ref, bi_attention_ref, contrastive_ref, window_attention_packed_ref
+    from oracle.blocks import (attention_ref, bi_attention_ref, contrastive_ref, window_attention_image_ref,
+                               window_attention_packed_ref)
 
     prev = mod.MSDeformAttnFunction
     mod.MSDeformAttnFunction = _OracleMSDA
@@ -25,6 +26,7 @@ def oracle_msda():
         with kernels.override("bi_attention", lambda q, k, vv, vl, pv=None, pl=None, p=0.0:
                               bi_attention_ref(q, k, vv, vl, pv, pl)), \
                 kernels.override("window_attention_packed", window_attention_packed_ref), \
+                kernels.override("window_attention_image", window_attention_image_ref), \
                 kernels.override("attention", lambda q, k, v, m=None, sc=None, p=0.0:
                                  attention_ref(q, k, v, m, sc)), \
                 kernels.override("contrastive_logits", contrastive_ref), \

@@ -194,6 +194,7 @@ t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 2, 300, 40))
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 1, 130, 256))
 t.test_emulated_window_attention(7, 3, 8, 4, True, torch.float32, 1e-5)
 t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
+t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.float32, 1e-5)
 t.test_emulated_attention(2, 2, 100, 130, 64, "bool", torch.float32, 1e-5, "lbh")
 print("sched-ok")
 """
@@ -235,6 +236,7 @@ t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
 t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
 t.test_emulated_msda_prologue(2, torch.bfloat16)
 t.test_emulated_msda_prologue(4, torch.float32)
+t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.bfloat16, 1.5e-2)
 """,
     r"""
 t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)
@@ -322,6 +324,58 @@ def test_emulated_window_attention_rejects_bad_shapes():
     big = torch.zeros(2, 81, 3, 1, 32)
     with pytest.raises(RuntimeError, match="bad sizes"):
         E.window_attn_forward(big, torch.zeros(289, 1), torch.zeros(81 * 81, dtype=torch.long), None, 1.0)
+
+
+@pytest.mark.parametrize("b,h,w,ws,shift,nH,bias,dtype,tol", [
+    (1, 9, 11, 7, 3, 3, True, torch.float32, 1e-5),    # shifted + padded both ways (Swin-T stage 0)
+    (2, 14, 14, 7, 0, 2, True, torch.float32, 1e-5),   # exact tiling, no shift: pure row map
+    (2, 14, 14, 7, 3, 2, False, torch.float32, 1e-5),  # shifted, no pad, no qkv bias
+    (1, 5, 9, 4, 2, 1, False, torch.float32, 1e-5),    # pad reads zeros (qkv_bias=False)
+    (1, 9, 11, 7, 3, 3, True, torch.bfloat16, 1.5e-2),
+    (2, 3, 10, 7, 0, 2, True, torch.bfloat16, 1.5e-2),  # H < window: one window row, mostly pad
+])
+def test_emulated_window_attention_image(b, h, w, ws, shift, nH, bias, dtype, tol):
+    """gd_window_attn_image_*: the pad / roll / partition / reverse / crop of
+    SwinTransformerBlock.forward fused into the kernel's row map, against
+    oracle.blocks.window_attention_image_ref in fp64 (the shift mask of
+    models' shifted_window_mask, i.e. the reference's :402-426 mask)."""
+    from models.GroundingDINO.backbone.swin_transformer import relative_position_index, shifted_window_mask
+    from oracle.blocks import window_attention_image_ref
+    g = torch.Generator().manual_seed(b * 1000 + h * 10 + w)
+    C = nH * 32
+    qkv = torch.randn(b, h * w, 3 * C, generator=g).to(dtype)
+    qb = (torch.randn(3 * C, generator=g) * 0.5).to(dtype) if bias else None
+    table = torch.randn((2 * ws - 1) ** 2, nH, generator=g) * 0.5
+    ridx = relative_position_index(ws, ws).reshape(-1)
+    hp, wp = -(-h // ws) * ws, -(-w // ws) * ws
+    mask = shifted_window_mask(hp, wp, ws, shift, "cpu") if shift else None
+    grad = torch.randn(b, h * w, C, generator=g).to(dtype)
+    scale = 32 ** -0.5
+    out, lse = E.window_attn_image_forward(qkv, qb, table, ridx, mask, (h, w), ws, shift, scale)
+    qd = qkv.double().requires_grad_(True)
+    bd = qb.double().requires_grad_(True) if bias else None
+    td = table.double().requires_grad_(True)
+    ref = window_attention_image_ref(qd, bd, td, ridx, None if mask is None else mask.double(), (h, w), ws, shift,
+                                     scale)
+    assert torch.isfinite(out.double()).all()  # every real token row written
+    assert E.rel_err(out.double(), ref.detach()) < tol
+    ref.backward(grad.double())
+    gq, gb, gt = E.window_attn_image_backward(qkv, qb, table, ridx, mask, (h, w), ws, shift, scale, out, lse, grad)
+    assert torch.isfinite(gq.double()).all()
+    assert E.rel_err(gq.double(), qd.grad) < tol * 2
+    assert E.rel_err(gt.double(), td.grad) < tol * 2
+    if bias:
+        assert E.rel_err(gb.double(), bd.grad) < tol * 2
+
+
+def test_emulated_window_attention_image_rejects_bad_geometry():
+    qkv = torch.zeros(1, 81, 96 * 3)
+    table, ridx = torch.zeros(169, 3), torch.zeros(49 * 49, dtype=torch.long)
+    with pytest.raises(RuntimeError, match="shift"):
+        E.window_attn_image_forward(qkv, None, table, ridx, None, (9, 9), 7, 7, 1.0)
+    with pytest.raises(RuntimeError, match="window 9"):
+        E.window_attn_image_forward(qkv, None, torch.zeros(289, 3), torch.zeros(81 * 81, dtype=torch.long), None,
+                                    (9, 9), 9, 0, 1.0)
 
 
 # ------------------------------- masked multi-head attention (flash, MFMA)

@@ -131,6 +131,80 @@ def test_window_attention_op_dispatch_and_fallback():
         assert _rel(out.cpu(), ref) < 1e-3, ws
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("b,h,w,ws,shift,nh,bias", [
+    (2, 25, 42, 7, 3, 3, True),   # Swin-T stage-0 geometry at 100x168 px: shifted, padded both ways
+    (1, 14, 21, 7, 0, 6, True),   # exact tiling, W-MSA
+    (1, 13, 9, 7, 3, 4, False),   # qkv_bias=False: pad rows read zeros
+])
+def test_window_attention_image_fwd_bwd(dtype, tol, b, h, w, ws, shift, nh, bias):
+    """The Swin block's pad / roll / partition / reverse / crop fused into the
+    window attention kernel (gd_window_attn_image_*), against the oracle's
+    step-by-step restatement in fp64, gradients of qkv, qkv bias and table."""
+    from gdino_amd.wattn import WindowAttnImageFunction
+    from models.GroundingDINO.backbone.swin_transformer import relative_position_index, shifted_window_mask
+    from oracle.blocks import window_attention_image_ref
+    g = torch.Generator().manual_seed(h * w + nh)
+    c = 32 * nh
+    qkv = torch.randn(b, h * w, 3 * c, generator=g).to(dtype)
+    qb = (torch.randn(3 * c, generator=g) * 0.5) if bias else None
+    table = torch.randn((2 * ws - 1) ** 2, nh, generator=g) * 0.5
+    ridx = relative_position_index(ws, ws).reshape(-1)
+    hp, wp = -(-h // ws) * ws, -(-w // ws) * ws
+    mask = shifted_window_mask(hp, wp, ws, shift, "cpu") if shift else None
+    grad = torch.randn(b, h * w, c, generator=g).to(dtype)
+    scale = 32 ** -0.5
+    qd = qkv.detach().double().requires_grad_(True)
+    bd = qb.to(dtype).double().requires_grad_(True) if bias else None
+    td = table.detach().double().requires_grad_(True)
+    ref = window_attention_image_ref(qd, bd, td, ridx, None if mask is None else mask.double(), (h, w), ws, shift,
+                                     scale)
+    ref.backward(grad.double())
+    qg = qkv.to(DEV).requires_grad_(True)
+    bg = qb.to(DEV).requires_grad_(True) if bias else None
+    tg = table.to(DEV).requires_grad_(True)
+    out = WindowAttnImageFunction.apply(qg, bg, tg, ridx.to(DEV), None if mask is None else mask.to(DEV), (h, w), ws,
+                                        shift, scale)
+    out.backward(grad.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert _rel(out.cpu(), ref.detach()) < tol
+    assert _rel(qg.grad.cpu(), qd.grad) < tol * 3
+    assert _rel(tg.grad.cpu(), td.grad) < tol * 3
+    if bias:
+        assert _rel(bg.grad.cpu(), bd.grad) < tol * 3
+
+
+def test_swin_block_fused_matches_windowed_path():
+    """SwinTransformerBlock.forward with the fused op vs the step-by-step
+    windowed path (_windowed_attention, the reference's sequence) on the GPU,
+    forward and parameter gradients, fp32."""
+    from models.GroundingDINO.backbone.swin_transformer import SwinTransformerBlock, shifted_window_mask
+    torch.manual_seed(0)
+    blk = SwinTransformerBlock(96, 3, 7, shift_size=3).to(DEV)
+    blk.H, blk.W = 19, 30
+    x = torch.randn(2, 19 * 30, 96, device=DEV)
+    mask = shifted_window_mask(21, 35, 7, 3, DEV)
+    res = {}
+    for fused in (True, False):
+        blk.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        if fused:
+            y = blk(xi, mask)
+        else:
+            sc = xi
+            t = blk._windowed_attention(blk.norm1(xi), mask)
+            t = sc + t
+            y = t + blk.mlp(blk.norm2(t))
+        y.square().mean().backward()
+        res[fused] = (y.detach(), xi.grad, {n: p.grad.clone() for n, p in blk.named_parameters()})
+    torch.cuda.synchronize()
+    assert _rel(res[True][0].cpu(), res[False][0].cpu()) < 1e-5
+    assert _rel(res[True][1].cpu(), res[False][1].cpu()) < 1e-4
+    for n in res[True][2]:
+        assert _rel(res[True][2][n].cpu(), res[False][2][n].cpu()) < 1e-4, n
+
+
 def test_window_attention_rejects_host_tensors():
     from gdino_amd.wattn import WindowAttnFunction
     qkv, table, ridx, mask = _wattn_inputs(7, 2, 4, 2, True, torch.float32)

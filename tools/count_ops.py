@@ -95,7 +95,8 @@ def main():
     # the GPU; the oracle restatements' own ops (forward and their autograd
     # backward) are not counted
     import models.GroundingDINO.ms_deform_attn as msda_mod
-    from oracle.blocks import attention_ref, bi_attention_ref, contrastive_ref, window_attention_packed_ref
+    from oracle.blocks import (attention_ref, bi_attention_ref, contrastive_ref, window_attention_image_ref,
+                               window_attention_packed_ref)
 
     def counted(fn, tag):
         class Op(torch.autograd.Function):
@@ -144,6 +145,9 @@ def main():
 
     win_op = counted(lambda qkv, t, r, m, sc: window_attention_packed_ref(qkv.float(), t.float(), r, m, sc)
                      .to(qkv.dtype), "gd.window_attn")
+    wimg_op = counted(lambda qkv, qb, t, r, m, hw, ws, sh, sc: window_attention_image_ref(
+        qkv.float(), None if qb is None else qb.float(), t.float(), r, m, hw, ws, sh, sc).to(qkv.dtype),
+        "gd.window_attn_image")
     attn_op = counted(lambda q, k, v, m, sc: attention_ref(q.float(), k.float(), v.float(), m, sc).to(q.dtype),
                       "gd.attn")
 
@@ -222,7 +226,8 @@ def main():
 
     try:
         with kernels.override("bi_attention", counted_bi), \
-                kernels.override("window_attention_packed", win_op), kernels.override("attention", counted_attn), \
+                kernels.override("window_attention_packed", win_op), kernels.override("window_attention_image", wimg_op), \
+                kernels.override("attention", counted_attn), \
                 kernels.override("contrastive_logits", con_op), kernels.override("contrastive_rowmax", counted_rowmax):
             step(Counter())  # warm-up (caches)
             with counter:
