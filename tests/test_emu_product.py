@@ -18,12 +18,29 @@ import emu_product
 import oracle_hooks
 
 
+def _off_cell_edges(model, std=0.01):
+    """The reference MSDA init (ms_deform_attn.py:198-221: zero
+    sampling_offsets weight, integer grid bias) puts every sampling point at
+    init exactly on a bilinear cell edge (pixel-centre reference + integer
+    pixel offset), where d(out)/d(loc) is one-sided and each implementation
+    picks a side by its own rounding of loc*size - 0.5 (the reference CUDA
+    kernel's, grid_sample's unnormalize, FMA contraction).  Both paths are
+    compared at a generic point instead: a small seeded perturbation of the
+    sampling_offsets weights (about 0.2 px), identical in both paths."""
+    g = torch.Generator().manual_seed(7)
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if n.endswith("sampling_offsets.weight"):
+                p.copy_(torch.randn(p.shape, generator=g) * std)
+
+
 def _step(mode, amp, hooks=None, size=(96, 128)):
     from gdino_amd import castcache, train
     from gdino_amd.config import make_args
     torch.manual_seed(0)
     args = make_args(device="cpu", num_queries=100)
     model, criterion, _, _ = train.build_training(args, "cpu")
+    _off_cell_edges(model)
     model.eval()
     samples, targets, captions, cats = train.synthetic_batch(1, size[0], size[1], n_boxes=3, n_tokens=24, seed=0,
                                                              device="cpu")
@@ -64,7 +81,7 @@ def test_train_step_fp32_emulated_hip_path_matches_oracle_path():
     assert _rel(pe[fin], po[fin]) < 1e-5
     assert set(go) == set(ge)
     worst = max((_rel(ge[n], go[n]), n) for n in go if go[n].norm() > 0)
-    assert worst[0] < 1e-4, worst
+    assert worst[0] < 1e-5, worst
 
 
 def _flat(o):
