@@ -150,13 +150,17 @@ def pmc_traffic(kname, bs):
     if not files:
         return None
     kind, lq = kname
-    units = bs * lq * 8  # N * Lq * M
-    grid = {"bwd": -(-units // 8) * 256, "fwd": -(-units // 64) * 256}[kind]  # threads (blocks x 256)
     with open(files[-1]) as f:
-        for k in json.load(f)["kernels"]:
-            if f"msda_{kind}" in k["kernel"] and k["grid"] == grid and k["traffic_bytes"] is not None:
-                return k["traffic_bytes"]
-    return None
+        rows = [k for k in json.load(f)["kernels"]
+                if f"msda_{kind}" in k["kernel"] and k["traffic_bytes"] is not None]
+    if not rows:
+        return None
+    # the launch grid is chosen inside the C-ABI (direct, lane32 or pixel-tiled
+    # backward), so match by size: the encoder call (Lq = S, tens of
+    # thousands of queries) has the largest grid of its kernel, the decoder
+    # call (Lq = 900) the smallest
+    pick = max if lq > 900 else min
+    return pick(rows, key=lambda k: k["grid"])["traffic_bytes"]
 
 
 def main(argv=None, device_type="cuda"):

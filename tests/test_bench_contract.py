@@ -90,3 +90,24 @@ def test_bench_two_ranks_contract():
     assert r0["n_gpus"] == 2 and r0["config"]["parallelism"] == "dp2" and r0["config"]["global_batch"] == 4
     assert abs(r0["value"] - 4 / (r0["ms_per_step"] / 1e3)) < 1e-6 * r0["value"]  # 2 images x 2 ranks per step
     assert "cpu_baseline" not in r0  # rank 0 at N=1 only
+
+
+def test_pmc_traffic_matches_the_encoder_and_decoder_launch_by_grid(tmp_path, monkeypatch):
+    """roofline.traffic: the committed PMC summary is matched by kernel name,
+    the encoder call to its kernel's largest grid, the decoder call to the
+    smallest (the C-ABI picks the backward variant, hence the grid)."""
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    rows = [{"kernel": "gd::msda_bwd_tiled<unsigned short, 64, 8>", "grid": 2_850_000, "traffic_bytes": 3.0e8},
+            {"kernel": "gd::msda_bwd_lane32<unsigned short, 4, 4>", "grid": 460_800, "traffic_bytes": 1.1e7},
+            {"kernel": "gd::msda_fwd_vec<unsigned short, 32, 4, 4>", "grid": 1_422_336, "traffic_bytes": 1.6e8},
+            {"kernel": "gd::msda_fwd_vec<unsigned short, 32, 4, 4>", "grid": 57_600, "traffic_bytes": None}]
+    (prof / "r01_pmc_traffic.json").write_text(json.dumps({"kernels": rows}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_traffic(("bwd", 22223), 2) == 3.0e8
+    assert bench.pmc_traffic(("bwd", 900), 2) == 1.1e7
+    assert bench.pmc_traffic(("fwd", 22223), 2) == 1.6e8
+    assert bench.pmc_traffic(("fwd", 900), 2) == 1.6e8  # only the measured row
+    (prof / "r01_pmc_traffic.json").write_text(json.dumps({"kernels": rows[2:3]}))
+    assert bench.pmc_traffic(("bwd", 22223), 2) is None
