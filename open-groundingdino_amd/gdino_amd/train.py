@@ -12,6 +12,7 @@ without the PAVE crop tiling (product-specific, out of scope):
 """
 from __future__ import annotations
 
+import functools
 import random
 from typing import List, Tuple
 
@@ -112,6 +113,31 @@ def build_optimizer(args, model):
 
 
 # -------------------------------------------------------------------- step
+_LOSS_WEIGHTS = {}
+
+
+def weighted_loss(loss_dict, weight_dict):
+    """sum(loss_dict[k] * weight_dict[k] for k in loss_dict if k in
+    weight_dict) (reference engine.py's total loss) as one stack, one
+    multiply by a cached on-device weight vector and one sum: 3 launches
+    instead of a multiply and an add per term (about 45 terms with the 5 aux
+    heads and the encoder head).  Each term's gradient is its weight exactly,
+    as in the per-term sum; only the rounding of the reported total differs."""
+    keys = [k for k in loss_dict if k in weight_dict]
+    if not keys or any(loss_dict[k].dim() for k in keys):
+        return sum(loss_dict[k] * weight_dict[k] for k in keys)
+    dt = functools.reduce(torch.promote_types, (loss_dict[k].dtype for k in keys), torch.float32)
+    vals = [loss_dict[k].to(dt) for k in keys]
+    dev = vals[0].device
+    ck = (tuple(keys), tuple(float(weight_dict[k]) for k in keys), dev, dt)
+    w = _LOSS_WEIGHTS.get(ck)
+    if w is None:
+        if len(_LOSS_WEIGHTS) > 16:
+            _LOSS_WEIGHTS.clear()
+        w = _LOSS_WEIGHTS[ck] = torch.tensor(ck[1], dtype=dt).to(dev)
+    return (torch.stack(vals) * w).sum()
+
+
 def train_step(model, criterion, optimizer, samples, targets, captions, cat_lists, clip_max_norm=0.1,
                amp_dtype=torch.bfloat16):
     """One optimisation step; returns the weighted loss tensor (not synced)."""
@@ -119,8 +145,7 @@ def train_step(model, criterion, optimizer, samples, targets, captions, cat_list
     with torch.autocast(device_type=dev_type, dtype=amp_dtype, enabled=amp_dtype is not None):
         outputs = model(samples, captions=captions)
         loss_dict = criterion(outputs, targets, cat_lists, captions)
-        wd = criterion.weight_dict
-        loss = sum(loss_dict[k] * wd[k] for k in loss_dict if k in wd)
+        loss = weighted_loss(loss_dict, criterion.weight_dict)
     optimizer.zero_grad(set_to_none=True)
     loss.backward()
     if clip_max_norm > 0:

@@ -154,8 +154,8 @@ def run_criterion(device="cpu", dtype=torch.float32):
                         spec.FOCAL_GAMMA, ["labels", "boxes"])
     outputs, leaves = spec.criterion_outputs(inp, device, dtype)
     losses = crit(outputs, inp["targets"], inp["cat_list"], inp["captions"])
-    wd = crit.weight_dict
-    total = sum(losses[k] * wd[k] for k in losses if k in wd)
+    from gdino_amd.train import weighted_loss
+    total = weighted_loss(losses, crit.weight_dict)  # the product's total (train_step)
     total.backward()
     res = {"loss." + k: v.detach() for k, v in losses.items()}
     res["total"] = total.detach()

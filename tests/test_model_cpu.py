@@ -239,3 +239,27 @@ def test_kernel_families_can_be_disabled(monkeypatch):
     assert not _lib.enabled("wattn") and not _lib.enabled("attn") and _lib.enabled("addln")
     monkeypatch.delenv("GDINO_DISABLE")
     assert _lib.enabled("wattn")
+
+
+def test_weighted_loss_matches_the_per_term_sum():
+    """train.weighted_loss (stack x cached weights, one sum) vs the reference
+    engine's sum(loss_dict[k] * weight_dict[k]): the same total to rounding,
+    every term's gradient exactly its weight, keys outside weight_dict
+    ignored, dtypes promoted (fp64 stays fp64)."""
+    from gdino_amd.train import weighted_loss
+    g = torch.Generator().manual_seed(0)
+    wd = {f"loss_{i}": float(w) for i, w in enumerate(torch.rand(45, generator=g) * 5)}
+    for dt in (torch.float32, torch.float64):
+        ld = {k: torch.rand((), generator=g, dtype=dt).requires_grad_(True) for k in wd}
+        ld["cardinality_error"] = torch.tensor(3.0, dtype=dt)
+        ld["loss_2"] = ld["loss_2"].detach().to(torch.bfloat16).requires_grad_(True)
+        ref = sum(ld[k] * wd[k] for k in ld if k in wd)
+        ref_promoted = sum(ld[k].to(dt) * wd[k] for k in ld if k in wd)  # the bf16 term's product in dt
+        tot = weighted_loss(ld, wd)
+        assert tot.dtype == dt
+        torch.testing.assert_close(tot, ref_promoted, rtol=1e-6, atol=0)
+        torch.testing.assert_close(tot, ref.to(dt), rtol=1e-4, atol=0)
+        grads = torch.autograd.grad(tot, [ld[k] for k in wd])
+        for k, gk in zip(wd, grads):
+            want = torch.tensor(wd[k], dtype=ld[k].dtype)
+            assert torch.equal(gk, want), k

@@ -212,8 +212,7 @@ def main():
             outputs = model(samples, captions=captions)
             c.phase = "criterion"
             loss_dict = criterion(outputs, targets, cats, captions)
-            wd = criterion.weight_dict
-            loss = sum(loss_dict[k] * wd[k] for k in loss_dict if k in wd)
+            loss = train.weighted_loss(loss_dict, criterion.weight_dict)
         optimizer.zero_grad(set_to_none=True)
         c.phase = "backward"
         loss.backward()
