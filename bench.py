@@ -178,7 +178,7 @@ def main(argv=None, device_type="cuda"):
         use_tunableop(a.tunableop)
     torch.manual_seed(1234 + rank)
 
-    from gdino_amd import msda
+    from gdino_amd import _lib, msda
     from gdino_amd.config import make_args
     from gdino_amd.train import build_training, synthetic_batch, train_step
 
@@ -264,7 +264,11 @@ def main(argv=None, device_type="cuda"):
                        "text_tokens": 256, "parallelism": f"dp{world}"},
             "roofline": roofline,
             "kernels": kernels,
-            "options": {"hip_graphs": bool(a.graphs), "tunableop": a.tunableop},
+            "options": {"hip_graphs": bool(a.graphs), "tunableop": a.tunableop,
+                        # HIP kernel families on this run (GDINO_DISABLE turns them off for A/B)
+                        "hip_families": ["msda", "biattn"] + [f for f in ("wattn", "attn", "contrastive", "prologue",
+                                                                         "wgrad", "addln") if _lib.enabled(f)],
+                        "msda_bwd": os.environ.get("GD_MSDA_BWD", "auto")},
             "loss": loss_v,
         }
         if not a.no_cpu_baseline and world == 1:
