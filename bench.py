@@ -227,6 +227,18 @@ def main(argv=None, device_type="cuda"):
         elapsed = float(t)
     loss_v = float(loss)
 
+    # one extra step, outside the timed region, with HIP events around every
+    # C-ABI call: device time per HIP entry point (all kernel families, not
+    # only the MSDA launches the roofline prices)
+    hip_calls = None
+    if on_gpu:
+        _lib.call_timer = _lib.CallTimer()
+        try:
+            train_step(model, criterion, optimizer, samples, targets, captions, cats)
+            hip_calls = _lib.call_timer.summary()
+        finally:
+            _lib.call_timer = None
+
     images = a.bs * world * a.steps
     value = images / elapsed
     # dominant MSDA launch = largest total time (none recorded when the
@@ -264,6 +276,7 @@ def main(argv=None, device_type="cuda"):
                        "text_tokens": 256, "parallelism": f"dp{world}"},
             "roofline": roofline,
             "kernels": kernels,
+            "hip_entry_points_one_step": hip_calls,
             "options": {"hip_graphs": bool(a.graphs), "tunableop": a.tunableop,
                         # HIP kernel families on this run (GDINO_DISABLE turns them off for A/B)
                         "hip_families": ["msda", "biattn"] + [f for f in ("wattn", "attn", "contrastive", "prologue",

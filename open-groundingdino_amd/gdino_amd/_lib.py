@@ -89,11 +89,51 @@ def register(name: str, argtypes) -> None:
         fn.restype = ctypes.c_int
 
 
+class CallTimer:
+    """HIP events around every C-ABI call, recorded on torch's current stream
+    (the stream every entry point is handed): launches and device time per
+    entry point.  bench.py runs one extra step after the timed region with
+    it, so the per-kernel figures cost the measured step nothing."""
+
+    def __init__(self):
+        self.records = []  # (entry point, start event, end event)
+
+    def begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, name, start):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.records.append((name, start, ev))
+
+    def summary(self):
+        """{entry point: {"calls": n, "total_ms": t, "avg_us": t / n}}"""
+        if self.records:
+            torch.cuda.synchronize()
+        out = {}
+        for name, s, e in self.records:
+            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0})
+            d["calls"] += 1
+            d["total_ms"] += s.elapsed_time(e)
+        for d in out.values():
+            d["avg_us"] = d["total_ms"] / d["calls"] * 1e3
+        return out
+
+
+call_timer = None  # set to a CallTimer to time every entry point
+
+
 def call(name: str, *args) -> None:
+    timer = call_timer
+    start = timer.begin() if timer is not None else None
     status = getattr(lib(), name)(*args)
     if status != GD_OK:
         msg = lib().gd_last_error().decode(errors="replace")
         raise GdError(f"{name}: status {status}: {msg}")
+    if timer is not None:
+        timer.end(name, start)
 
 
 def runtime_info() -> str:

@@ -76,3 +76,49 @@ def test_msda_module_is_a_drop_in_for_the_reference_extension():
     assert len([p for p in fwd if p.default is inspect.Parameter.empty]) <= 6 <= len(fwd)
     assert len([p for p in bwd if p.default is inspect.Parameter.empty]) <= 7 <= len(bwd)
     assert [p.name for p in bwd[5:7]] == ["grad_output", "im2col_step"]
+
+
+def test_call_timer_brackets_every_entry_point(monkeypatch):
+    """_lib.CallTimer (bench.py's per-entry-point pass): events recorded
+    before and after each C-ABI call, summed per entry point; a failing call
+    still raises and records nothing."""
+    import itertools
+
+    import torch
+
+    from gdino_amd import _lib
+
+    clock = itertools.count()
+
+    class FakeEvent:
+        def __init__(self, enable_timing=False):
+            assert enable_timing
+
+        def record(self):
+            self.t = next(clock)
+
+        def elapsed_time(self, other):
+            return float(other.t - self.t)
+
+    class FakeLib:
+        def gd_a(self, *args):
+            return _lib.GD_OK
+
+        def gd_bad(self, *args):
+            return _lib.GD_OK + 1
+
+        def gd_last_error(self):
+            return b"boom"
+
+    fake = FakeLib()
+    monkeypatch.setattr(torch.cuda, "Event", FakeEvent)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(_lib, "lib", lambda: fake)
+    monkeypatch.setattr(_lib, "call_timer", _lib.CallTimer())
+    for _ in range(3):
+        _lib.call("gd_a", 1, 2)
+    with pytest.raises(_lib.GdError, match="boom"):
+        _lib.call("gd_bad")
+    s = _lib.call_timer.summary()
+    assert set(s) == {"gd_a"}
+    assert s["gd_a"]["calls"] == 3 and s["gd_a"]["total_ms"] == 3.0 and s["gd_a"]["avg_us"] == 1000.0
