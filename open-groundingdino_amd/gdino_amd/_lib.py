@@ -96,36 +96,47 @@ class CallTimer:
     it, so the per-kernel figures cost the measured step nothing."""
 
     def __init__(self):
-        self.records = []  # (entry point, start event, end event)
+        self.records = []  # (entry point, start event, end event, algorithmic flops or None)
 
     def begin(self):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         return ev
 
-    def end(self, name, start):
+    def end(self, name, start, flops=None):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        self.records.append((name, start, ev))
+        self.records.append((name, start, ev, flops))
 
     def summary(self):
-        """{entry point: {"calls": n, "total_ms": t, "avg_us": t / n}}"""
+        """{entry point: {"calls": n, "total_ms": t, "avg_us": t / n}}, plus
+        for the MFMA entry points (those given algorithmic flops) "tflops" and
+        "mfma_frac" against the dense bf16 MFMA peak."""
         if self.records:
             torch.cuda.synchronize()
         out = {}
-        for name, s, e in self.records:
-            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0})
+        for name, s, e, flops in self.records:
+            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0, "flops": 0.0 if flops is not None else None})
             d["calls"] += 1
             d["total_ms"] += s.elapsed_time(e)
+            if flops is not None and d["flops"] is not None:
+                d["flops"] += flops
         for d in out.values():
             d["avg_us"] = d["total_ms"] / d["calls"] * 1e3
+            fl = d.pop("flops")
+            if fl is not None and d["total_ms"] > 0:
+                d["tflops"] = fl / (d["total_ms"] * 1e-3) / 1e12
+                d["mfma_frac"] = d["tflops"] * 1e12 / MFMA_BF16_PEAK
         return out
 
 
 call_timer = None  # set to a CallTimer to time every entry point
+MFMA_BF16_PEAK = 2.5e15  # FLOP/s, dense bf16 (MI355X_MICROARCH.md chip table)
 
 
-def call(name: str, *args) -> None:
+def call(name: str, *args, flops: float | None = None) -> None:
+    """Run entry point ``name``; raise GdError on a non-OK status.  ``flops``
+    (algorithmic, MFMA entry points only) feeds CallTimer's TFLOP/s."""
     timer = call_timer
     start = timer.begin() if timer is not None else None
     status = getattr(lib(), name)(*args)
@@ -133,7 +144,7 @@ def call(name: str, *args) -> None:
         msg = lib().gd_last_error().decode(errors="replace")
         raise GdError(f"{name}: status {status}: {msg}")
     if timer is not None:
-        timer.end(name, start)
+        timer.end(name, start, flops)
 
 
 def runtime_info() -> str:

@@ -87,7 +87,8 @@ class AttnFunction(torch.autograd.Function):
         lse = torch.empty(b, h, lq, dtype=torch.float32, device=q.device)
         _lib.call("gd_attn_forward", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
                   _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), kind, ms, float(scale), float(dropout_p), int(seed),
-                  out.data_ptr(), _st3(out), lse.data_ptr(), _lib.stream_of(q))
+                  out.data_ptr(), _st3(out), lse.data_ptr(), _lib.stream_of(q),
+                  flops=4.0 * b * h * lq * lk * hd)  # S = QK^T, O = PV
         ctx.save_for_backward(q, k, v, m, out, lse)
         ctx.kind, ctx.ms, ctx.scale = kind, tuple(ms) if ms is not None else None, float(scale)
         ctx.dropout_p, ctx.seed = float(dropout_p), int(seed)
@@ -106,7 +107,8 @@ class AttnFunction(torch.autograd.Function):
         _lib.call("gd_attn_backward", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
                   _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), ctx.kind, ms, ctx.scale, ctx.dropout_p, ctx.seed,
                   out.data_ptr(), _st3(out), dout.data_ptr(), _st3(dout), lse.data_ptr(), dsum.data_ptr(),
-                  dq.data_ptr(), _st3(dq), dk.data_ptr(), _st3(dk), dv.data_ptr(), _st3(dv), _lib.stream_of(q))
+                  dq.data_ptr(), _st3(dq), dk.data_ptr(), _st3(dk), dv.data_ptr(), _st3(dv), _lib.stream_of(q),
+                  flops=10.0 * b * h * lq * lk * hd)  # S recompute, dP, dV, dQ, dK (2.5x forward)
         return dq, dk, dv, None, None, None, None
 
 

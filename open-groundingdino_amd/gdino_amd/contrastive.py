@@ -54,7 +54,7 @@ def _launch(xc, tc, keep, tout, logits, rowmax):
     t = tc.shape[1]
     _lib.call("gd_contrastive_forward", _lib.dtype_code(xc), xc.data_ptr(), (ctypes.c_int64 * 2)(*xc.stride()[:2]),
               tc.data_ptr(), (ctypes.c_int64 * 2)(*tc.stride()[:2]), keep.data_ptr(), b, q, t, c, tout,
-              _lib.ptr(logits), _lib.ptr(rowmax), _lib.stream_of(xc))
+              _lib.ptr(logits), _lib.ptr(rowmax), _lib.stream_of(xc), flops=2.0 * b * q * t * c)
 
 
 def supported(x, text, max_text_len) -> bool:

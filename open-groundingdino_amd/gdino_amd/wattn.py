@@ -67,7 +67,7 @@ class WindowAttnFunction(torch.autograd.Function):
         lse = torch.empty(b_, nh, n, dtype=torch.float32, device=qkv.device)
         _lib.call("gd_window_attn_forward", _lib.dtype_code(qkv), qkv.data_ptr(), table32.data_ptr(),
                   ridx.data_ptr(), _lib.ptr(mask32), b_, n, nh, hd, nw, float(scale), out.data_ptr(),
-                  lse.data_ptr(), _lib.stream_of(qkv))
+                  lse.data_ptr(), _lib.stream_of(qkv), flops=4.0 * b_ * nh * n * n * hd)
         ctx.save_for_backward(qkv, table32, ridx, mask32, out, lse)
         ctx.scale = float(scale)
         ctx.table_dtype = table.dtype
@@ -83,7 +83,8 @@ class WindowAttnFunction(torch.autograd.Function):
         dtable = torch.zeros_like(table32)
         _lib.call("gd_window_attn_backward", _lib.dtype_code(qkv), qkv.data_ptr(), table32.data_ptr(),
                   ridx.data_ptr(), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), b_, n, nh,
-                  hd, nw, ctx.scale, dqkv.data_ptr(), dtable.data_ptr(), _lib.stream_of(qkv))
+                  hd, nw, ctx.scale, dqkv.data_ptr(), dtable.data_ptr(), _lib.stream_of(qkv),
+                  flops=10.0 * b_ * nh * n * n * hd)
         return dqkv, dtable.to(ctx.table_dtype), None, None, None
 
 
@@ -124,7 +125,8 @@ class WindowAttnImageFunction(torch.autograd.Function):
         lse = torch.empty(b * (hp // ws) * (wp // ws), nh, ws * ws, dtype=torch.float32, device=qkv.device)
         _lib.call("gd_window_attn_image_forward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
                   table32.data_ptr(), ridx.data_ptr(), _lib.ptr(mask32), b, hw[0], hw[1], ws, shift, nh, hd,
-                  float(scale), out.data_ptr(), lse.data_ptr(), _lib.stream_of(qkv))
+                  float(scale), out.data_ptr(), lse.data_ptr(), _lib.stream_of(qkv),
+                  flops=4.0 * lse.numel() * ws * ws * hd)  # windows x heads x N^2 x hd
         ctx.save_for_backward(qkv, bias, table32, ridx, mask32, out, lse)
         ctx.geo = (hw, ws, shift, float(scale))
         ctx.dtypes = (None if qkv_bias is None else qkv_bias.dtype, table.dtype)
@@ -143,7 +145,8 @@ class WindowAttnImageFunction(torch.autograd.Function):
         _lib.call("gd_window_attn_image_backward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
                   table32.data_ptr(), ridx.data_ptr(), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(),
                   lse.data_ptr(), b, hw[0], hw[1], ws, shift, nh, c3 // (3 * nh), scale, dqkv.data_ptr(),
-                  _lib.ptr(dbias), dtable.data_ptr(), _lib.stream_of(qkv))
+                  _lib.ptr(dbias), dtable.data_ptr(), _lib.stream_of(qkv),
+                  flops=10.0 * lse.numel() * ws * ws * c3 // (3 * nh))
         bias_dt, table_dt = ctx.dtypes
         return (dqkv, None if dbias is None else dbias.to(bias_dt), dtable.to(table_dt),
                 None, None, None, None, None, None)

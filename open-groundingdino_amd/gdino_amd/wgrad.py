@@ -63,7 +63,7 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, want_bias: bool):
     dw = torch.empty(o, i, dtype=torch.float32, device=dy2.device)
     db = torch.empty(o, dtype=torch.float32, device=dy2.device) if want_bias else None
     _lib.call("gd_wgrad", _lib.dtype_code(dy2), dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), t, o, i,
-              s, ws.data_ptr(), dw.data_ptr(), _lib.ptr(db), _lib.stream_of(dy2))
+              s, ws.data_ptr(), dw.data_ptr(), _lib.ptr(db), _lib.stream_of(dy2), flops=2.0 * t * o * i)
     return dw, db
 
 
@@ -89,7 +89,7 @@ def tn_matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     out = torch.empty(nb, o, i, dtype=a.dtype, device=a.device)
     _lib.call("gd_wgrad_batched", _lib.dtype_code(a2), a2.data_ptr(), a2.stride(1), a2.stride(0), b2.data_ptr(),
               b2.stride(1), b2.stride(0), t, o, i, nb, s, ws.data_ptr(), _lib.dtype_code(out), out.data_ptr(),
-              out.stride(0), None, _lib.stream_of(a2))
+              out.stride(0), None, _lib.stream_of(a2), flops=2.0 * nb * t * o * i)
     return out.reshape(*lead, o, i)
 
 

@@ -104,6 +104,9 @@ def test_call_timer_brackets_every_entry_point(monkeypatch):
         def gd_a(self, *args):
             return _lib.GD_OK
 
+        def gd_mfma(self, *args):
+            return _lib.GD_OK
+
         def gd_bad(self, *args):
             return _lib.GD_OK + 1
 
@@ -119,6 +122,11 @@ def test_call_timer_brackets_every_entry_point(monkeypatch):
         _lib.call("gd_a", 1, 2)
     with pytest.raises(_lib.GdError, match="boom"):
         _lib.call("gd_bad")
+    _lib.call("gd_mfma", flops=1e12)
+    _lib.call("gd_mfma", flops=2e12)
     s = _lib.call_timer.summary()
-    assert set(s) == {"gd_a"}
+    assert set(s) == {"gd_a", "gd_mfma"}
     assert s["gd_a"]["calls"] == 3 and s["gd_a"]["total_ms"] == 3.0 and s["gd_a"]["avg_us"] == 1000.0
+    assert "tflops" not in s["gd_a"]
+    # 3e12 flops in 2 ms = 1500 TFLOP/s, 0.6 of the 2.5 PFLOP/s dense bf16 peak
+    assert s["gd_mfma"]["tflops"] == pytest.approx(1500.0) and s["gd_mfma"]["mfma_frac"] == pytest.approx(0.6)
