@@ -96,47 +96,55 @@ class CallTimer:
     it, so the per-kernel figures cost the measured step nothing."""
 
     def __init__(self):
-        self.records = []  # (entry point, start event, end event, algorithmic flops or None)
+        self.records = []  # (entry point, start event, end event, algorithmic flops, algorithmic bytes)
 
     def begin(self):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         return ev
 
-    def end(self, name, start, flops=None):
+    def end(self, name, start, flops=None, nbytes=None):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        self.records.append((name, start, ev, flops))
+        self.records.append((name, start, ev, flops, nbytes))
 
     def summary(self):
         """{entry point: {"calls": n, "total_ms": t, "avg_us": t / n}}, plus
         for the MFMA entry points (those given algorithmic flops) "tflops" and
-        "mfma_frac" against the dense bf16 MFMA peak."""
+        "mfma_frac" against the dense bf16 MFMA peak, and for the HBM-bound
+        ones (given algorithmic bytes) "GBps" and "hbm_frac" against 8 TB/s."""
         if self.records:
             torch.cuda.synchronize()
         out = {}
-        for name, s, e, flops in self.records:
-            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0, "flops": 0.0 if flops is not None else None})
+        for name, s, e, flops, nbytes in self.records:
+            d = out.setdefault(name, {"calls": 0, "total_ms": 0.0, "flops": 0.0 if flops is not None else None,
+                                      "bytes": 0.0 if nbytes is not None else None})
             d["calls"] += 1
             d["total_ms"] += s.elapsed_time(e)
-            if flops is not None and d["flops"] is not None:
-                d["flops"] += flops
+            for key, v in (("flops", flops), ("bytes", nbytes)):
+                d[key] = d[key] + v if (v is not None and d[key] is not None) else None
         for d in out.values():
             d["avg_us"] = d["total_ms"] / d["calls"] * 1e3
-            fl = d.pop("flops")
-            if fl is not None and d["total_ms"] > 0:
-                d["tflops"] = fl / (d["total_ms"] * 1e-3) / 1e12
-                d["mfma_frac"] = d["tflops"] * 1e12 / MFMA_BF16_PEAK
+            fl, nb = d.pop("flops"), d.pop("bytes")
+            sec = d["total_ms"] * 1e-3
+            if fl is not None and sec > 0:
+                d["tflops"] = fl / sec / 1e12
+                d["mfma_frac"] = fl / sec / MFMA_BF16_PEAK
+            if nb is not None and sec > 0:
+                d["GBps"] = nb / sec / 1e9
+                d["hbm_frac"] = nb / sec / HBM_PEAK
         return out
 
 
 call_timer = None  # set to a CallTimer to time every entry point
 MFMA_BF16_PEAK = 2.5e15  # FLOP/s, dense bf16 (MI355X_MICROARCH.md chip table)
+HBM_PEAK = 8.0e12  # B/s, same table
 
 
-def call(name: str, *args, flops: float | None = None) -> None:
+def call(name: str, *args, flops: float | None = None, nbytes: float | None = None) -> None:
     """Run entry point ``name``; raise GdError on a non-OK status.  ``flops``
-    (algorithmic, MFMA entry points only) feeds CallTimer's TFLOP/s."""
+    (MFMA entry points) and ``nbytes`` (HBM-bound ones), both algorithmic,
+    feed CallTimer's TFLOP/s and GB/s."""
     timer = call_timer
     start = timer.begin() if timer is not None else None
     status = getattr(lib(), name)(*args)
@@ -144,7 +152,7 @@ def call(name: str, *args, flops: float | None = None) -> None:
         msg = lib().gd_last_error().decode(errors="replace")
         raise GdError(f"{name}: status {status}: {msg}")
     if timer is not None:
-        timer.end(name, start, flops)
+        timer.end(name, start, flops, nbytes)
 
 
 def runtime_info() -> str:

@@ -54,7 +54,8 @@ class BiSoftmax(torch.autograd.Function):
         ws = _workspace(b, h, n, t, s.device)
         mv, ml = _u8(pad_v), _u8(pad_l)
         _lib.call("gd_biattn_softmax_fwd", _lib.dtype_code(s), s.data_ptr(), _lib.ptr(mv), _lib.ptr(ml),
-                  b, h, n, t, pv.data_ptr(), pl.data_ptr(), ws.data_ptr(), _lib.stream_of(s))
+                  b, h, n, t, pv.data_ptr(), pl.data_ptr(), ws.data_ptr(), _lib.stream_of(s),
+                  nbytes=3.0 * s.numel() * s.element_size())  # read S, write P_v and P_l
         ctx.save_for_backward(pv, pl)
         return pv, pl
 
@@ -67,7 +68,8 @@ class BiSoftmax(torch.autograd.Function):
         ds = torch.empty_like(pv)
         ws = _workspace(b, h, n, t, pv.device)
         _lib.call("gd_biattn_softmax_bwd", _lib.dtype_code(pv), pv.data_ptr(), pl.data_ptr(), dpv.data_ptr(),
-                  dpl.data_ptr(), b, h, n, t, ds.data_ptr(), ws.data_ptr(), _lib.stream_of(pv))
+                  dpl.data_ptr(), b, h, n, t, ds.data_ptr(), ws.data_ptr(), _lib.stream_of(pv),
+                  nbytes=5.0 * pv.numel() * pv.element_size())  # read P_v, P_l, dP_v, dP_l; write dS
         return ds, None, None
 
 

@@ -52,7 +52,8 @@ class AddLayerNormFunction(torch.autograd.Function):
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
         _lib.call("gd_add_layernorm_forward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(r), r.data_ptr(),
                   weight.data_ptr(), bias.data_ptr(), rows, c, float(eps), y.data_ptr(), mean.data_ptr(),
-                  rstd.data_ptr(), _lib.stream_of(x))
+                  rstd.data_ptr(), _lib.stream_of(x),
+                  nbytes=rows * (c * (x.element_size() + r.element_size() + 4) + 8))  # x, r -> y, mean, rstd
         ctx.save_for_backward(x, r, weight, mean, rstd)
         return y
 
@@ -70,7 +71,9 @@ class AddLayerNormFunction(torch.autograd.Function):
         ws = _workspace(c, x.device) if want_wb else None
         _lib.call("gd_add_layernorm_backward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(r), r.data_ptr(),
                   weight.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, c, dx.data_ptr(),
-                  _lib.ptr(dr), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws), _lib.stream_of(x))
+                  _lib.ptr(dr), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws), _lib.stream_of(x),
+                  nbytes=rows * (c * (2 * x.element_size() + r.element_size() + 4
+                                      + (r.element_size() if dr is not None else 0)) + 8))
         return (dx if ctx.needs_input_grad[0] else None, dr, dw if ctx.needs_input_grad[2] else None,
                 db if ctx.needs_input_grad[3] else None, None)
 

@@ -104,6 +104,9 @@ def test_call_timer_brackets_every_entry_point(monkeypatch):
         def gd_a(self, *args):
             return _lib.GD_OK
 
+        def gd_hbm(self, *args):
+            return _lib.GD_OK
+
         def gd_mfma(self, *args):
             return _lib.GD_OK
 
@@ -124,9 +127,13 @@ def test_call_timer_brackets_every_entry_point(monkeypatch):
         _lib.call("gd_bad")
     _lib.call("gd_mfma", flops=1e12)
     _lib.call("gd_mfma", flops=2e12)
+    _lib.call("gd_a", nbytes=1e9)  # bytes given on some calls only: no GB/s
+    _lib.call("gd_hbm", nbytes=4e9)
     s = _lib.call_timer.summary()
-    assert set(s) == {"gd_a", "gd_mfma"}
-    assert s["gd_a"]["calls"] == 3 and s["gd_a"]["total_ms"] == 3.0 and s["gd_a"]["avg_us"] == 1000.0
+    assert set(s) == {"gd_a", "gd_mfma", "gd_hbm"}
+    assert "GBps" not in s["gd_a"] and "GBps" not in s["gd_mfma"]
+    assert s["gd_hbm"]["GBps"] == pytest.approx(4000.0) and s["gd_hbm"]["hbm_frac"] == pytest.approx(0.5)
+    assert s["gd_a"]["calls"] == 4 and s["gd_a"]["total_ms"] == 4.0 and s["gd_a"]["avg_us"] == 1000.0
     assert "tflops" not in s["gd_a"]
     # 3e12 flops in 2 ms = 1500 TFLOP/s, 0.6 of the 2.5 PFLOP/s dense bf16 peak
     assert s["gd_mfma"]["tflops"] == pytest.approx(1500.0) and s["gd_mfma"]["mfma_frac"] == pytest.approx(0.6)
