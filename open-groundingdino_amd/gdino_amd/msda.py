@@ -102,12 +102,13 @@ def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_lo
     (N, S, M, D, L, Lq, P), loc, attn = _check(value, spatial_shapes, level_start_index,
                                                sampling_loc, attn_weight, im2col_step)
     out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+    nbytes = algorithmic_bytes("fwd", N, S, M, D, L, Lq, P, value.element_size())
     t0 = timer.begin() if timer is not None else None
     _lib.call("gd_msda_forward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
               level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), N, S, M, D, L, Lq, P,
-              out.data_ptr(), _lib.stream_of(value))
+              out.data_ptr(), _lib.stream_of(value), nbytes=nbytes)
     if t0 is not None:
-        timer.end("fwd", Lq, algorithmic_bytes("fwd", N, S, M, D, L, Lq, P, value.element_size()), t0)
+        timer.end("fwd", Lq, nbytes, t0)
     return out
 
 
@@ -140,13 +141,14 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     hs = None
     if host_shapes is not None and len(host_shapes) == L:
         hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
+    nbytes = algorithmic_bytes("bwd", N, S, M, D, L, Lq, P, value.element_size())
     t0 = timer.begin() if timer is not None else None
     _lib.call("gd_msda_backward_geom", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
               level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), grad_output.data_ptr(),
               N, S, M, D, L, Lq, P, grad_value.data_ptr(), grad_loc.data_ptr(), grad_attn.data_ptr(),
-              hs, _lib.stream_of(value))
+              hs, _lib.stream_of(value), nbytes=nbytes)
     if t0 is not None:
-        timer.end("bwd", Lq, algorithmic_bytes("bwd", N, S, M, D, L, Lq, P, value.element_size()), t0)
+        timer.end("bwd", Lq, nbytes, t0)
     out_dtype = value.dtype if grad_value_dtype is None else grad_value_dtype
     if grad_value.dtype != out_dtype:
         grad_value = grad_value.to(out_dtype)
