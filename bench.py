@@ -236,6 +236,8 @@ def main(argv=None, device_type="cuda"):
         try:
             train_step(model, criterion, optimizer, samples, targets, captions, cats)
             hip_calls = _lib.call_timer.summary()
+        except Exception as e:  # diagnostics only: never cost the bench line
+            hip_calls = {"error": repr(e)[:300]}
         finally:
             _lib.call_timer = None
 
