@@ -42,17 +42,52 @@
 namespace gd {
 namespace {
 #include "msda_kernels.inc"
+#include "msda_enc.inc"
 
 constexpr int kTileQ = 32;      // queries per workgroup (one head)
 constexpr int kTileRows = 384;  // LDS accumulator rows (48 KB): 3 workgroups per CU
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// GD_MSDA_BWD=lane32 forces the round-1 kernel (A/B measurements; read per
-// call so a test can compare both kernels in one process).
-inline bool tiled_bwd_enabled() {
+// Encoder-shape backward selection, read per call so a test can compare the
+// kernels in one process (GD_MSDA_BWD):
+//   lane32  direct 128-B atomics for every corner (msda_bwd_lane32);
+//   tiled   round-1 LDS pre-aggregation over 4 x 8 pixel blocks
+//           (msda_bwd_tiled; 3.77 ms vs lane32's 2.19 ms on the box);
+//   enc     2-D query tiles per level, vector lanes, packed LDS boxes
+//           (msda_bwd_enc, msda_enc.inc);
+//   auto / unset: see bwd_variant().
+enum class BwdVariant { kLane32, kTiled, kEnc };
+inline BwdVariant bwd_variant() {
   const char* e = getenv("GD_MSDA_BWD");
-  return !(e && strcmp(e, "lane32") == 0);
+  if (e && strcmp(e, "tiled") == 0) return BwdVariant::kTiled;
+  if (e && strcmp(e, "enc") == 0) return BwdVariant::kEnc;
+  return BwdVariant::kLane32;
+}
+
+// msda_bwd_enc geometry (tuning overrides, default below):
+//   GD_MSDA_ENC_TILE="THxTW,THxTW,THxTW,THxTW"  query tile extents per query level
+//   GD_MSDA_ENC_CAP="r0,r1,r2,r3"               LDS rows of each sampled level's box
+inline void enc_geometry(int (&th)[4], int (&tw)[4], int (&cap)[4]) {
+  static const int dth[4] = {8, 8, 4, 4}, dtw[4] = {16, 8, 8, 8}, dcap[4] = {224, 96, 64, 64};
+  for (int l = 0; l < 4; ++l) { th[l] = dth[l]; tw[l] = dtw[l]; cap[l] = dcap[l]; }
+  if (const char* e = getenv("GD_MSDA_ENC_TILE")) {
+    int v[8];
+    if (sscanf(e, "%dx%d,%dx%d,%dx%d,%dx%d", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6], &v[7]) == 8)
+      for (int l = 0; l < 4; ++l)
+        if (v[2 * l] > 0 && v[2 * l + 1] > 0) { th[l] = v[2 * l]; tw[l] = v[2 * l + 1]; }
+  }
+  if (const char* e = getenv("GD_MSDA_ENC_CAP")) {
+    int v[4];
+    if (sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4)
+      for (int l = 0; l < 4; ++l)
+        if (v[l] >= 0) cap[l] = v[l];
+  }
+}
+
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
 }
 
 inline int grid_for(int64_t total, int block) {
@@ -152,7 +187,55 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
   // the value rows, so consecutive queries sample neighbouring rows): tiled
   // backward with LDS pre-aggregation.  Cross-attention (the decoder's 900
   // score-sorted queries) keeps the direct-atomic kernel.
-  if ((dt == GD_F32 || dt == GD_BF16) && lane_ok && Lq == S && tiled_bwd_enabled()) {
+  const BwdVariant variant = bwd_variant();
+  if ((dt == GD_F32 || dt == GD_BF16) && lane_ok && Lq == S && variant == BwdVariant::kEnc && shapes_host &&
+      aligned16(value) && aligned16(grad_out) && aligned16(attn) && aligned16(grad_attn)) {
+    EncTiles tl{};
+    int th[4], tw[4], cap[4];
+    enc_geometry(th, tw, cap);
+    int64_t cover = 0, nt = 0;
+    int rows = 0;
+    bool ok = true;
+    for (int l = 0; l < L; ++l) {
+      const int64_t h = shapes_host[2 * l], w = shapes_host[2 * l + 1];
+      ok = ok && h > 0 && w > 0;
+      cover += h * w;
+      tl.th[l] = th[l];
+      tl.tw[l] = tw[l];
+      tl.tx[l] = int((w + tw[l] - 1) / tw[l]);
+      tl.tstart[l] = int(nt);
+      nt += ((h + th[l] - 1) / th[l]) * tl.tx[l];
+      tl.rbase[l] = rows;
+      tl.rcap[l] = cap[l];
+      rows += cap[l];
+    }
+    tl.tstart[4] = int(nt);
+    const int64_t blocks = int64_t(N) * nt * M;
+    if (ok && cover == S && blocks < (int64_t(1) << 31) && rows <= 1024) {
+      const int rmax = env_int("GD_MSDA_ENC_RMAX", 8);
+      const int mode = env_int("GD_MSDA_ENC_MODE", 0);  // 1: ds_add_f32 instead of read-modify-write
+#define GD_ENC_LAUNCH(T, NR)                                                                           \
+  hipLaunchKernelGGL((msda_bwd_enc<T, NR>), dim3(int(blocks)), dim3(128), 0, s, (const T*)value, shapes, \
+                     lsi, (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_value,   \
+                     (float*)grad_loc, (float*)grad_attn, S, M, tl, rmax, mode)
+#define GD_ENC_LAUNCH_ROWS(T)                  \
+  if (rows <= 160) GD_ENC_LAUNCH(T, 160);      \
+  else if (rows <= 256) GD_ENC_LAUNCH(T, 256); \
+  else if (rows <= 512) GD_ENC_LAUNCH(T, 512); \
+  else GD_ENC_LAUNCH(T, 1024)
+      if (dt == GD_F32) {
+        GD_ENC_LAUNCH_ROWS(float);
+        GD_LAUNCH_CHECK("msda_bwd_enc<f32>");
+      } else {
+        GD_ENC_LAUNCH_ROWS(uint16_t);
+        GD_LAUNCH_CHECK("msda_bwd_enc<bf16>");
+      }
+#undef GD_ENC_LAUNCH_ROWS
+#undef GD_ENC_LAUNCH
+      return GD_OK;
+    }
+  }
+  if ((dt == GD_F32 || dt == GD_BF16) && lane_ok && Lq == S && variant == BwdVariant::kTiled) {
     // 2-D pixel tiles when the host knows the level grid (and it covers the
     // S queries exactly); otherwise strips of kTileQ consecutive queries
     int tiles_per_n = (Lq + kTileQ - 1) / kTileQ, tiles2d = 0;

@@ -213,6 +213,9 @@ inline V shfl_xor(V v, int mask, int width) {
   return xchg_from(v, wave_base() + src);
 }
 
+// v_readlane: lane `src` of the caller's wave (a wave-uniform result)
+inline int readlane(int v, int src) { return xchg_from(v, wave_base() + unsigned(src)); }
+
 // All 64 lanes of the caller's wave contribute `nbytes` (<= 64) and every
 // lane receives the 64 contributions in lane order (MFMA operand exchange).
 inline void wave_gather(const void* mine, size_t nbytes, void* all) {
@@ -309,6 +312,7 @@ void launch(dim3 g, dim3 b, F&& f) {
 #define blockDim (::gd_emu::grid().block)
 #define __syncthreads() ::gd_emu::syncthreads()
 #define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
+#define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
 #define __builtin_amdgcn_ds_swizzle(v, pattern) ::gd_emu::ds_swizzle((v), (pattern))
 #define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) \
   ::gd_emu::update_dpp((old), (src), (ctrl), (rm), (bm), (bc))
@@ -322,5 +326,19 @@ template <typename T>
 inline T atomicAdd(T* p, T v) {
   const T old = *p;
   *p = old + v;
+  return old;
+}
+
+template <typename T>
+inline T atomicMin(T* p, T v) {
+  const T old = *p;
+  *p = v < old ? v : old;
+  return old;
+}
+
+template <typename T>
+inline T atomicMax(T* p, T v) {
+  const T old = *p;
+  *p = v > old ? v : old;
   return old;
 }

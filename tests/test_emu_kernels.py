@@ -94,7 +94,8 @@ def test_emulated_verified_kernels_match_oracle(vdtype, tol):
     (MEDIUM, 1, False, 0.0),    # uniform points: boxes overflow, global fallback
     (WIDE, 1, True, 0.02),
 ])
-def test_emulated_tiled_backward_matches_oracle(levels, n, local, outliers):
+def test_emulated_tiled_backward_matches_oracle(levels, n, local, outliers, monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     S = sum(h * w for h, w in levels)
     inputs = _levels_inputs(levels, n, S, seed=S + n, local=local, outlier_frac=outliers)
     _check_bwd(inputs, 1e-5)
@@ -106,7 +107,8 @@ def test_emulated_tiled_backward_matches_oracle(levels, n, local, outliers):
     (MEDIUM, 2, True, 0.1),
     (WIDE, 1, True, 0.02),
 ])
-def test_emulated_pixel_block_tiles_match_oracle(levels, n, local, outliers):
+def test_emulated_pixel_block_tiles_match_oracle(levels, n, local, outliers, monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     """gd_msda_backward_geom: 4 x 8 pixel-block tiles of each level (host
     level shapes given) -- same sums as the oracle and the strip tiling."""
     S = sum(h * w for h, w in levels)
@@ -117,22 +119,66 @@ def test_emulated_pixel_block_tiles_match_oracle(levels, n, local, outliers):
     assert torch.equal(blocks[1], strips[1]) and torch.equal(blocks[2], strips[2])
 
 
-def test_emulated_geom_falls_back_when_levels_do_not_tile_the_queries():
+def test_emulated_geom_falls_back_when_levels_do_not_tile_the_queries(monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     S = sum(h * w for h, w in MEDIUM)
     inputs = _levels_inputs(MEDIUM, 1, S, seed=21, local=True)
     wrong = [(h, w + 1) for h, w in MEDIUM]  # covers more than S: strip tiling
     _check_bwd(inputs, 1e-5, host_shapes=wrong)
 
 
-def test_emulated_tiled_backward_bf16():
+def test_emulated_tiled_backward_bf16(monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     S = sum(h * w for h, w in MEDIUM)
     inputs = _levels_inputs(MEDIUM, 2, S, seed=5, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
     _check_bwd(inputs, 1e-5)  # bf16-exact inputs, fp32 accumulation
 
 
+# ------------------------------ encoder backward: 2-D tiles, packed LDS boxes
+ENC_TILES = ["16x16,8x8,4x4,2x4", "4x16,3x8,2x4,1x4", "5x7,3x3,2x2,1x1"]
+
+
+@pytest.mark.parametrize("levels,n,local,outliers,spread", [
+    (SMALL, 1, True, 0.0, 2.0),     # every level box fits
+    (MEDIUM, 2, True, 0.0, 2.0),    # tail tiles on every level, batch boundary inside the grid
+    (MEDIUM, 2, True, 0.1, 2.0),    # + outliers: clipped boxes, mixed LDS / global atomics
+    (MEDIUM, 1, False, 0.0, 2.0),   # uniform points: boxes clipped to the footprint window
+    (WIDE, 1, True, 0.02, 6.0),     # wide spread: boxes overflow the accumulator
+])
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+def test_emulated_enc_backward_matches_oracle(levels, n, local, outliers, spread, vdtype, monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "enc")
+    S = sum(h * w for h, w in levels)
+    inputs = _levels_inputs(levels, n, S, seed=S + 3 * n, vdtype=vdtype, local=local, spread_px=spread,
+                            outlier_frac=outliers)
+    _check_bwd(inputs, 1e-5, host_shapes=levels)  # bf16-exact inputs, fp32 accumulation
+
+
+@pytest.mark.parametrize("tiles", ENC_TILES)
+@pytest.mark.parametrize("cap,rmax", [("224,96,64,64", 8), ("40,16,8,0", 2), ("500,300,100,100", 0)])
+def test_emulated_enc_backward_tilings(tiles, cap, rmax, monkeypatch):
+    """Any tile extents, LDS region sizes and clip radius give the same sums."""
+    monkeypatch.setenv("GD_MSDA_BWD", "enc")
+    monkeypatch.setenv("GD_MSDA_ENC_TILE", tiles)
+    monkeypatch.setenv("GD_MSDA_ENC_CAP", cap)
+    monkeypatch.setenv("GD_MSDA_ENC_RMAX", str(rmax))
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=17, local=True, outlier_frac=0.05)
+    _check_bwd(inputs, 1e-5, host_shapes=MEDIUM)
+
+
+def test_emulated_enc_without_host_shapes_uses_direct_kernel(monkeypatch):
+    """gd_msda_backward (no level shapes on the host): the direct kernel."""
+    monkeypatch.setenv("GD_MSDA_BWD", "enc")
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 1, S, seed=23, local=True)
+    _check_bwd(inputs, 1e-5)
+
+
 def test_emulated_tiled_equals_direct_atomic_kernel(monkeypatch):
     S = sum(h * w for h, w in MEDIUM)
     inputs = _levels_inputs(MEDIUM, 2, S, seed=9, local=True, outlier_frac=0.05)
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     tiled = E.msda_backward(*inputs)
     monkeypatch.setenv("GD_MSDA_BWD", "lane32")
     direct = E.msda_backward(*inputs)
@@ -228,6 +274,13 @@ t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=3, local=True, outlier_frac=0
 t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 37, seed=6), 1e-5)
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=8, local=True, outlier_frac=0.02), 1e-5,
              host_shapes=t.WIDE)
+import os
+for v in ("enc", "tiled"):
+    os.environ["GD_MSDA_BWD"] = v
+    t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=5, local=True, outlier_frac=0.1), 1e-5, host_shapes=t.MEDIUM)
+    t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=9, local=True, spread_px=6.0,
+                                  outlier_frac=0.02, vdtype=torch.bfloat16), 1e-5, host_shapes=t.WIDE)
+del os.environ["GD_MSDA_BWD"]
 """,
     r"""
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)

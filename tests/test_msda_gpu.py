@@ -229,26 +229,32 @@ def _check_bwd_vs_oracle(inputs, tol, host_shapes=None):
                                       ([(13, 21), (7, 11), (4, 6), (2, 3)], 2),  # tail tile, n boundary
                                       ([(40, 67), (20, 34), (10, 17), (5, 9)], 2)])
 @pytest.mark.parametrize("outliers", [0.0, 0.05])
-def test_encoder_tiled_backward_small(levels, n, outliers):
+def test_encoder_tiled_backward_small(levels, n, outliers, monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     _check_bwd_vs_oracle(_encoder_inputs(levels, n, seed=len(levels) + n, vdtype=torch.float32,
                                          outlier_frac=outliers), 1e-3)
 
 
 @pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
-def test_encoder_tiled_backward_800x1333(vdtype, tol):
+def test_encoder_tiled_backward_800x1333(vdtype, tol, monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     _check_bwd_vs_oracle(_encoder_inputs(LEVELS_800, 2, seed=7, vdtype=vdtype, outlier_frac=0.01), tol)
 
 
 @pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
-def test_encoder_pixel_block_backward_800x1333(vdtype, tol):
-    """gd_msda_backward_geom (host level shapes -> 4 x 8 pixel-block tiles),
-    the path the model's encoder takes."""
+@pytest.mark.parametrize("variant", ["tiled", "auto", "enc"])
+def test_encoder_pixel_block_backward_800x1333(vdtype, tol, variant, monkeypatch):
+    """gd_msda_backward_geom (host level shapes -> 4 x 8 pixel-block tiles
+    with GD_MSDA_BWD=tiled), the path the model's encoder takes."""
+    monkeypatch.setenv("GD_MSDA_BWD", variant)
     _check_bwd_vs_oracle(_encoder_inputs(LEVELS_800, 2, seed=8, vdtype=vdtype, outlier_frac=0.01), tol,
                          host_shapes=LEVELS_800)
 
 
 @pytest.mark.parametrize("levels", [[(6, 9), (3, 5), (2, 3), (1, 2)], [(13, 21), (7, 11), (4, 6), (2, 3)]])
-def test_encoder_pixel_block_backward_small(levels):
+@pytest.mark.parametrize("variant", ["tiled", "enc"])
+def test_encoder_pixel_block_backward_small(levels, variant, monkeypatch):
+    monkeypatch.setenv("GD_MSDA_BWD", variant)
     _check_bwd_vs_oracle(_encoder_inputs(levels, 2, seed=3, vdtype=torch.float32, outlier_frac=0.05), 1e-3,
                          host_shapes=levels)
 
@@ -257,6 +263,7 @@ def test_encoder_tiled_matches_direct_atomic_kernel(monkeypatch):
     """Same sums, different order: the LDS-aggregated kernel against the
     round-1 direct-atomic kernel (GD_MSDA_BWD=lane32) on one input."""
     inputs = [t.to(DEV) for t in _encoder_inputs(LEVELS_800, 2, seed=11, vdtype=torch.float32)]
+    monkeypatch.setenv("GD_MSDA_BWD", "tiled")
     tiled = _msda().ms_deform_attn_backward(*inputs, 64)
     monkeypatch.setenv("GD_MSDA_BWD", "lane32")
     direct = _msda().ms_deform_attn_backward(*inputs, 64)
@@ -266,6 +273,75 @@ def test_encoder_tiled_matches_direct_atomic_kernel(monkeypatch):
     # compiler's FMA contraction choices in the two kernels)
     torch.testing.assert_close(tiled[1], direct[1], rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(tiled[2], direct[2], rtol=1e-6, atol=1e-7)
+
+
+ENC_TILINGS = [None, "8x16,8x8,4x4,2x4", "4x16,3x8,2x4,1x4", "5x7,3x3,2x2,1x1"]
+
+
+@pytest.mark.parametrize("tiles", ENC_TILINGS)
+@pytest.mark.parametrize("cap,rmax", [("224,96,64,64", 8), ("40,16,8,0", 4), ("500,300,100,100", 0)])
+@pytest.mark.parametrize("spread,outliers", [(2.0, 0.01), (6.0, 0.05)])
+def test_encoder_enc_backward_tilings_800x1333(tiles, cap, rmax, spread, outliers, monkeypatch):
+    """msda_bwd_enc (2-D query tiles per level, one LDS box per sampled
+    level): any tile extents, region sizes and clip radius give the oracle's
+    sums, including wide offsets whose boxes overflow their region (global
+    fallback)."""
+    monkeypatch.setenv("GD_MSDA_BWD", "enc")
+    monkeypatch.setenv("GD_MSDA_ENC_CAP", cap)
+    monkeypatch.setenv("GD_MSDA_ENC_RMAX", str(rmax))
+    if tiles:
+        monkeypatch.setenv("GD_MSDA_ENC_TILE", tiles)
+    _check_bwd_vs_oracle(_encoder_inputs(LEVELS_800, 2, seed=31, vdtype=torch.float32, spread_px=spread,
+                                         outlier_frac=outliers), 1e-3, host_shapes=LEVELS_800)
+
+
+def _init_geometry_loc(levels, n):
+    """The reference initialisation's encoder sampling locations
+    (ms_deform_attn.py:198-221: zero offset weights, per-head direction x
+    (point + 1) pixel biases): every point lands (up to fp32 rounding) on an
+    integer pixel coordinate, so floor() sits on a cell edge -- the geometry
+    the train-step bench runs at."""
+    import math
+    M, P = 8, 4
+    refs = []
+    for (h, w) in levels:
+        yy, xx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+        refs.append(torch.stack([(xx.reshape(-1) + 0.5) / w, (yy.reshape(-1) + 0.5) / h], -1))
+    ref = torch.cat(refs)
+    ang = torch.arange(M, dtype=torch.float32) * (2 * math.pi / M)
+    d = torch.stack([ang.cos(), ang.sin()], -1)
+    d = d / d.abs().max(-1, keepdim=True).values
+    off = d[:, None, :] * torch.arange(1, P + 1, dtype=torch.float32)[None, :, None]
+    wh = torch.as_tensor([(w, h) for (h, w) in levels], dtype=torch.float32)
+    loc = ref[:, None, None, None, :] + off[None, :, None, :, :] / wh[None, None, :, None, :]
+    return loc[None].expand(n, -1, -1, -1, -1, -1).contiguous()
+
+
+@pytest.mark.parametrize("variant", ["lane32", "tiled", "enc"])
+@pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+def test_encoder_backward_init_geometry_800x1333(variant, vdtype, tol, monkeypatch):
+    """Sampling points on cell edges (the reference init): a kernel that
+    evaluates loc * W - 0.5 twice (e.g. for a pipelined gather and again for
+    the weights) can floor the two results to different cells."""
+    monkeypatch.setenv("GD_MSDA_BWD", variant)
+    value, shapes, lsi, _, attn, grad_out = _encoder_inputs(LEVELS_800, 2, seed=41, vdtype=vdtype)
+    loc = _init_geometry_loc(LEVELS_800, 2)
+    _check_bwd_vs_oracle((value, shapes, lsi, loc, attn, grad_out), tol, host_shapes=LEVELS_800)
+
+
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+def test_encoder_enc_matches_direct_atomic_kernel(vdtype, monkeypatch):
+    """Same sums, different order: msda_bwd_enc against msda_bwd_lane32 on
+    one input (fp32 accumulation in both)."""
+    inputs = [t.to(DEV) for t in _encoder_inputs(LEVELS_800, 2, seed=13, vdtype=vdtype)]
+    monkeypatch.setenv("GD_MSDA_BWD", "enc")
+    enc = _msda().ms_deform_attn_backward(*inputs, 64, grad_value_dtype=torch.float32, host_shapes=LEVELS_800)
+    monkeypatch.setenv("GD_MSDA_BWD", "lane32")
+    direct = _msda().ms_deform_attn_backward(*inputs, 64, grad_value_dtype=torch.float32, host_shapes=LEVELS_800)
+    torch.testing.assert_close(enc[0], direct[0], rtol=1e-4, atol=1e-5)
+    # grad_attn: per-lane dot products summed in a different order
+    torch.testing.assert_close(enc[2], direct[2], rtol=1e-4, atol=1e-5)
+    assert _rel_err_gl(enc[1].cpu(), direct[1].double().cpu().numpy(), inputs[3].cpu(), inputs[1].cpu()) < 1e-5
 
 
 # ------------------------------------------------------------- edge/contract

@@ -1,36 +1,74 @@
 #!/usr/bin/env bash
 # One GPU session on a fresh MI355X box (run through gpurun from the repo root):
-#   gpurun --timeout 1200 -- bash tools/gpu_session.sh [core|ab|tune|graphs]
+#   gpurun --timeout 1200 -- bash tools/gpu_session.sh <mode>
 # Every GPU step has its own time limit and the steps are chained with &&:
 # the first failure ends the session (no retries, no further GPU work).
-# Logs and profiler output go to gpurun_out/ (copy the summaries that are to
-# be judged into profiles/ afterwards).
+# Small logs go to gpurun_out/ (merged back, <= 64 MiB); raw profiler output
+# stays in /tmp on the box and only its summaries are copied to gpurun_out/.
 set -euo pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 MODE="${1:-core}"
 T() { timeout -k 10 "$@"; }
+step() { echo "[$(date +%T)] $*"; }
+PROF=/tmp/gd_prof
+
+# rocprofv3 kernel trace of a short bench run; summaries only
+prof_trace() {  # name, bench args...
+  local name=$1; shift
+  step "rocprof kernel trace: $name"
+  T 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/$name" -o run -- \
+      python3 bench.py --no-cpu-baseline "$@" > "gpurun_out/${name}.log" 2>&1
+  mkdir -p "gpurun_out/$name"
+  find "$PROF/$name" -name '*stats*.csv' -exec cp {} "gpurun_out/$name/" \;
+  local kt; kt=$(find "$PROF/$name" -name '*kernel_trace.csv' | head -n 1 || true)
+  if [ -n "$kt" ]; then
+    python3 tools/trace_steps.py --skip 2 "$kt" > "gpurun_out/$name/steady_state.txt" 2>&1 || true
+  fi
+}
+# one PMC pass (one counter group per run)
+prof_pmc() {  # name, counters, bench args...
+  local name=$1 counters=$2; shift 2
+  step "rocprof pmc $counters: $name"
+  T 600 rocprofv3 --pmc $counters --kernel-trace --output-format csv -d "$PROF/$name" -o run -- \
+      python3 bench.py --no-cpu-baseline "$@" > "gpurun_out/${name}.log" 2>&1
+}
 
 case "$MODE" in
+tests)
+  step "pytest -m gpu"
+  T 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > gpurun_out/s_gpu_tests.log 2>&1
+  ;;
+bench)
+  step "bench (default)"
+  T 600 python3 bench.py > gpurun_out/s_bench.log 2>&1 && tail -c 600 gpurun_out/s_bench.log
+  ;;
 core)
-  # 1) parity on the HIP path, 2) the default bench line, 3) A/B of the
-  # host-overhead switches, 4) kernel trace of the default bench, 5/6) HBM
-  # traffic counters in their own passes (FETCH_SIZE and WRITE_SIZE do not
-  # fit one TCC pass; MI355X_MICROARCH.md "rocprofv3 PMC slots")
-  T 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/s_gpu_tests.log 2>&1 &&
+  # parity, the default bench line, A/B of the encoder backward, the kernel
+  # trace, and HBM traffic counters in their own passes (FETCH_SIZE and
+  # WRITE_SIZE do not fit one TCC pass; MI355X_MICROARCH.md "rocprofv3 PMC")
+  step "pytest -m gpu"
+  T 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > gpurun_out/s_gpu_tests.log 2>&1 &&
+  step "bench (default)" &&
   T 600 python3 bench.py > gpurun_out/s_bench.log 2>&1 &&
-  GDINO_CAST_CACHE=0 GDINO_FUSE_PROJ=0 T 600 python3 bench.py --no-cpu-baseline \
-      > gpurun_out/s_bench_nocache.log 2>&1 &&
-  T 600 rocprofv3 --kernel-trace --stats -d gpurun_out/s_prof -o run -- \
-      python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline > gpurun_out/s_prof.log 2>&1 &&
-  T 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/s_pmc_fetch -o run -- \
-      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_fetch.log 2>&1 &&
-  T 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/s_pmc_write -o run -- \
-      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/s_pmc_write.log 2>&1 &&
-  # 7) host-only: per-launch bytes per (kernel, grid); copy the JSON to
-  # profiles/rNN_pmc_traffic.json so bench.py's roofline carries `traffic`
-  python3 tools/pmc_traffic.py --fetch gpurun_out/s_pmc_fetch --write gpurun_out/s_pmc_write \
+  step "bench (tiled encoder backward)" &&
+  GD_MSDA_BWD=tiled T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_bench_tiled.log 2>&1 &&
+  prof_trace s_prof --steps 3 --warmup 2 &&
+  prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&
+  prof_pmc s_pmc_write WRITE_SIZE --steps 1 --warmup 1 &&
+  step "pmc_traffic" &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
+      --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
+  ;;
+prof)
+  prof_trace s_prof --steps 3 --warmup 2 &&
+  prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&
+  prof_pmc s_pmc_write WRITE_SIZE --steps 1 --warmup 1 &&
+  step "pmc_traffic" &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
       --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
   ;;
 tune)
@@ -41,23 +79,23 @@ tune)
   ;;
 ab)
   # A/B of every kernel family against its torch composition (GDINO_DISABLE)
-  # and of the MSDA backward against the round-1 kernel: one bench line each
   T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_ab_all.log 2>&1 &&
   for fam in wattn attn contrastive prologue wgrad addln; do
     GDINO_DISABLE=$fam T 600 python3 bench.py --no-cpu-baseline > "gpurun_out/s_ab_no_$fam.log" 2>&1 || exit $?
   done &&
-  GD_MSDA_BWD=lane32 T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_ab_msda_lane32.log 2>&1 &&
   GDINO_DISABLE=wattn,attn,contrastive,prologue,wgrad,addln T 600 python3 bench.py --no-cpu-baseline \
       > gpurun_out/s_ab_none.log 2>&1
   ;;
 graphs)
-  # HIP-graph replay (experimental; faulted in round 1 before MIOpen was
-  # removed from the captured region): run alone, in its own gpurun call
+  # HIP-graph replay (experimental): run alone, in its own gpurun call
   GDINO_GRAPH_DEBUG=1 T 600 python3 bench.py --no-cpu-baseline --graphs --steps 5 --warmup 2 \
       > gpurun_out/s_bench_graphs.log 2>&1
   ;;
 *)
-  echo "usage: $0 [core|ab|tune|graphs]" >&2
+  echo "usage: $0 [tests|bench|core|prof|tune|ab|graphs]" >&2
   exit 2
   ;;
 esac
+rc=$?
+step "done rc=$rc"; du -sh gpurun_out
+exit $rc

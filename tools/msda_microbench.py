@@ -64,10 +64,92 @@ def time_it(fn, iters=20, warm=3):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
+def init_geometry_loc(n, dev="cuda"):
+    """Encoder sampling locations of the reference initialisation
+    (ms_deform_attn.py:198-221: zero offset weights, per-head direction x
+    (point + 1) pixel biases on every level) -- the step-0 geometry the
+    train-step bench runs at."""
+    import math
+    M, L, P = 8, 4, 4
+    ys, xs = [], []
+    for (h, w) in LEVELS:
+        yy, xx = torch.meshgrid(torch.arange(h, device=dev), torch.arange(w, device=dev), indexing="ij")
+        ys.append((yy.reshape(-1) + 0.5) / h)
+        xs.append((xx.reshape(-1) + 0.5) / w)
+    ref = torch.stack([torch.cat(xs), torch.cat(ys)], -1)  # [S, 2]
+    ang = torch.arange(M, device=dev, dtype=torch.float32) * (2 * math.pi / M)
+    d = torch.stack([ang.cos(), ang.sin()], -1)
+    d = d / d.abs().max(-1, keepdim=True).values
+    off = d[:, None, :] * torch.arange(1, P + 1, device=dev, dtype=torch.float32)[None, :, None]  # [M, P, 2]
+    wh = torch.as_tensor([(w, h) for (h, w) in LEVELS], device=dev, dtype=torch.float32)  # [L, 2]
+    loc = ref[:, None, None, None, :] + off[None, :, None, :, :] / wh[None, None, :, None, :]
+    return loc[None].expand(n, -1, -1, -1, -1, -1).contiguous()
+
+
+ENC_VARIANTS = [
+    ("lane32", {"GD_MSDA_BWD": "lane32"}),
+    ("enc default", {"GD_MSDA_BWD": "enc"}),
+    ("enc 8x8 r256", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x8,8x8,4x8,4x8", "GD_MSDA_ENC_CAP": "128,64,32,32"}),
+    ("enc 8x16 r256", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x16,8x8,4x8,4x8",
+                       "GD_MSDA_ENC_CAP": "160,48,24,24"}),
+    ("enc 4x8 r256", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "96,64,48,48"}),
+    ("enc 4x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "80,32,24,24"}),
+    ("enc 4x16 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x16,4x8,4x4,4x4",
+                       "GD_MSDA_ENC_CAP": "96,32,16,16"}),
+    ("enc 8x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "96,32,16,16"}),
+    ("enc 4x8 r256 dsadd", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4",
+                            "GD_MSDA_ENC_CAP": "96,64,48,48", "GD_MSDA_ENC_MODE": "1"}),
+    ("enc 8x16 r256 dsadd", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x16,8x8,4x8,4x8",
+                             "GD_MSDA_ENC_CAP": "160,48,24,24", "GD_MSDA_ENC_MODE": "1"}),
+]
+ENC_PROBES = []
+
+
+def enc_variants(iters, variants=None):
+    """Encoder-shape backward (bs=2, 800x1333, bf16 value) under every
+    kernel variant, on the init geometry and on a 2-px random spread; each
+    variant checked against lane32 on the same inputs."""
+    S = sum(h * w for h, w in LEVELS)
+    variants = variants or ENC_VARIANTS
+    for geom in ("init", "spread2"):
+        v, sh, ls, loc, attn, go = inputs(S, torch.bfloat16)
+        if geom == "init":
+            loc = init_geometry_loc(2)
+        ref = None
+        for name, env in variants:
+            saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_ENC_RMAX", "GD_MSDA_ENC_CAP",
+                                                    "GD_MSDA_ENC_TILE", "GD_MSDA_ENC_MODE")}
+            for k in saved:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            try:
+                fn = lambda: msda.ms_deform_attn_backward(v, sh, ls, loc, attn, go, 64,  # noqa: E731
+                                                          grad_value_dtype=torch.float32, host_shapes=LEVELS)
+                out = fn()
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = [t.clone() for t in out]
+                err = [float((a - b).abs().max() / b.abs().max()) for a, b in zip(out, ref)]
+                t = time_it(fn, iters)
+            finally:
+                for k, val in saved.items():
+                    os.environ.pop(k, None)
+                    if val is not None:
+                        os.environ[k] = val
+            bb = algo_bytes(2, S, S, 2, bwd=True)
+            print(json.dumps(dict(geom=geom, variant=name, bwd_us=t * 1e6, bwd_GBps=bb / t / 1e9,
+                                  frac=bb / t / PEAK, rel_err_vs_lane32=err)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--enc-variants", action="store_true")
+    ap.add_argument("--enc-probes", action="store_true")
     args = ap.parse_args()
+    if args.enc_variants or args.enc_probes:
+        enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[2]] + ENC_PROBES if args.enc_probes else None)
+        return
     S = sum(h * w for h, w in LEVELS)
     res = []
     for lq, tag in ((S, "enc"), (900, "dec")):
