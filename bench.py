@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -49,6 +50,8 @@ def parse(argv=None):
     ap.add_argument("--backbone", default="swin_T_224_1k")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--forward-only", action="store_true",
+                    help="BASELINE config 2: eval-mode forward (no autograd) instead of the train step")
     ap.add_argument("--graphs", action="store_true",
                     help="replay forward_core (fwd+bwd) as HIP graphs (experimental, 1 GPU; DESIGN.md §7)")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
@@ -79,64 +82,95 @@ def setup_dist(n, on_gpu=True):
     return dist.get_rank(), dist.get_world_size(), local
 
 
-def cpu_baseline(bs):
-    """Time the reference MSDA CPU fallback (oracle restatement of
-    ms_deform_attn_core_pytorch) on this host for the per-step MSDA work of
-    one rank, bounded to a few seconds: one encoder-shape fwd, one encoder
-    fwd+bwd, one decoder fwd+bwd at bs images, then scale by the per-step
-    counts (6 enc fwd recomputed + 6 enc fwd+bwd + 6 dec fwd+bwd)."""
-    import platform
-
-    from oracle.msda_torch import msda_grid_sample
-
-    g = torch.Generator().manual_seed(0)
-    shapes = torch.as_tensor(LEVELS_800, dtype=torch.long)
-    S = int(shapes.prod(1).sum())
-    M, D, L, P = 8, 32, 4, 4
-
-    def case(lq, bwd):
-        v = torch.rand(bs, S, M, D, generator=g).requires_grad_(bwd)
-        loc = torch.rand(bs, lq, M, L, P, 2, generator=g).requires_grad_(bwd)
-        a = torch.rand(bs, lq, M, L, P, generator=g)
-        a = (a / a.sum((-1, -2), keepdim=True)).requires_grad_(bwd)
-        t0 = time.perf_counter()
-        out = msda_grid_sample(v, shapes, loc, a)
-        if bwd:
-            out.sum().backward()
-        return time.perf_counter() - t0
-
-    def per_step_time():
-        t = (case(S, False), case(S, True), case(900, True))
-        return t, 6 * sum(t)
-
-    (t_enc_f, t_enc_fb, t_dec_fb), per_step = per_step_time()
-    threads = torch.get_num_threads()
-    # SURVEY 8d: also at one thread (the reference fallback's scalar rate)
-    torch.set_num_threads(1)
-    try:
-        (s_enc_f, s_enc_fb, s_dec_fb), per_step_1 = per_step_time()
-    finally:
-        torch.set_num_threads(threads)
-    model = "unknown"
+def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
-        model = platform.processor()
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(bs):
+    """The reference's pure-PyTorch MSDA CPU fallback (oracle restatement of
+    ms_deform_attn_core_pytorch, oracle/msda_torch.py) timed on this host by
+    BASELINE.md section 3's protocol: cfg1 (N=1, 512x512 levels, Lq=100) fwd
+    and fwd+bwd with 5 warmups + 20 reps; the bs=2 800x1333 encoder layer
+    (Lq = S = 22 223) fwd and fwd+bwd and the decoder layer (Lq=900) fwd+bwd
+    with fewer reps (the encoder case is 0.4-2.5 s per call: 2 warmups + 5
+    reps); median and p90 of each, at 1 thread and at the process's thread
+    count.  `value` converts the all-thread medians to images/s of the train
+    step's MSDA share (6 encoder fwd recomputed under activation
+    checkpointing + 6 encoder fwd+bwd + 6 decoder fwd+bwd per step)."""
+    import statistics
+
+    from oracle.msda_torch import msda_grid_sample
+
+    M, D, L, P = 8, 32, 4, 4
+
+    def make(levels, n, lq, seed):
+        g = torch.Generator().manual_seed(seed)
+        shapes = torch.as_tensor(levels, dtype=torch.long)
+        S = int(shapes.prod(1).sum())
+        v = torch.rand(n, S, M, D, generator=g)
+        loc = torch.rand(n, lq, M, L, P, 2, generator=g)
+        a = torch.rand(n, lq, M, L, P, generator=g) + 1e-5
+        a = a / a.sum((-1, -2), keepdim=True)
+        return shapes, v, loc, a
+
+    def timed(inputs, bwd, warm, reps):
+        shapes, v0, loc0, a0 = inputs
+        ts = []
+        for i in range(warm + reps):
+            v, loc, a = (t.clone().requires_grad_(bwd) for t in (v0, loc0, a0))
+            t0 = time.perf_counter()
+            out = msda_grid_sample(v, shapes, loc, a)
+            if bwd:
+                out.backward(torch.ones_like(out))
+            dt = time.perf_counter() - t0
+            if i >= warm:
+                ts.append(dt)
+        ts.sort()
+        return {"median_s": statistics.median(ts), "p90_s": ts[min(len(ts) - 1, int(0.9 * len(ts)))],
+                "reps": reps, "warmup": warm}
+
+    cfg1 = make([(64, 64), (32, 32), (16, 16), (8, 8)], 1, 100, 0)
+    enc = make(LEVELS_800, bs, sum(h * w for h, w in LEVELS_800), 1)
+    dec = make(LEVELS_800, bs, 900, 2)
+    cases = [("cfg1_fwd", cfg1, False, 5, 20), ("cfg1_fwd_bwd", cfg1, True, 5, 20),
+             ("enc_fwd", enc, False, 2, 5), ("enc_fwd_bwd", enc, True, 2, 5), ("dec_fwd_bwd", dec, True, 3, 10)]
+    threads = torch.get_num_threads()
+    res = {}
+    for nt in (threads, 1):
+        torch.set_num_threads(nt)
+        try:
+            res[nt] = {name: timed(inp, bwd, w, r) for name, inp, bwd, w, r in cases}
+        finally:
+            torch.set_num_threads(threads)
+
+    def per_step(r):
+        return 6 * (r["enc_fwd"]["median_s"] + r["enc_fwd_bwd"]["median_s"] + r["dec_fwd_bwd"]["median_s"])
+
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
     return {
-        "value": bs / per_step,
+        "value": bs / per_step(res[threads]),
         "unit": "images/s (MSDA fwd+bwd share of the train step only)",
         "cores": threads,
         "kind": "port",
-        "single_thread": {"value": bs / per_step_1, "cores": 1,
-                          "sample": f"same calls at 1 thread: {s_enc_f:.2f}s / {s_enc_fb:.2f}s / {s_dec_fb:.2f}s"},
-        "sample": (f"reference pure-PyTorch MSDA fallback (grid_sample restatement, oracle/msda_torch.py) "
-                   f"on {model}, os.cpu_count()={os.cpu_count()}: 1x encoder fwd {t_enc_f:.2f}s, "
-                   f"1x encoder fwd+bwd {t_enc_fb:.2f}s, 1x decoder fwd+bwd {t_dec_fb:.2f}s at bs={bs} "
-                   f"800x1333, scaled x6 each to one train step ({per_step:.1f}s)"),
+        "single_thread": {"value": bs / per_step(res[1]), "cores": 1},
+        "cases": {f"{nt}thr": {k: {kk: round(vv, 6) if isinstance(vv, float) else vv for kk, vv in d.items()}
+                               for k, d in r.items()} for nt, r in res.items()},
+        "sample": (f"reference pure-PyTorch MSDA fallback (grid_sample restatement, oracle/msda_torch.py) on "
+                   f"{_cpu_model()}, torch threads={threads}, affinity cpus={affinity}, "
+                   f"os.cpu_count()={os.cpu_count()}: cfg1 (N=1, 512x512, Lq=100) and bs={bs} 800x1333 encoder / "
+                   f"decoder layers, median of timed reps after warmups; value = {bs} images / (6 x (enc fwd + "
+                   f"enc fwd+bwd + dec fwd+bwd)) = {per_step(res[threads]):.2f} s of MSDA per step"),
     }
 
 
@@ -180,12 +214,12 @@ def main(argv=None, device_type="cuda"):
 
     from gdino_amd import _lib, msda
     from gdino_amd.config import make_args
-    from gdino_amd.train import build_training, synthetic_batch, train_step
+    from gdino_amd.train import build_training, forward_step, synthetic_batch, train_step
 
     args = make_args(device=str(device), backbone=a.backbone)
     model, criterion, _, optimizer = build_training(args, device)
-    model.train()
-    if world > 1:
+    model.train(not a.forward_only)
+    if world > 1 and not a.forward_only:
         # reference main.py:258-261 (DDP + static graph); buckets sized for
         # xGMI rings (fewer, larger all-reduces), launched as backward
         # produces them so RCCL overlaps the rest of the backward pass
@@ -193,9 +227,18 @@ def main(argv=None, device_type="cuda"):
             model, device_ids=[local] if on_gpu else None, bucket_cap_mb=a.bucket_mb, static_graph=True)
     samples, targets, captions, cats = synthetic_batch(a.bs, a.height, a.width, n_boxes=8, n_tokens=256,
                                                        seed=1000 + rank, device=device)
+    if a.forward_only:
+        def step():
+            out = forward_step(model, samples, captions)
+            return out["pred_logits"].float().nan_to_num(0.0, 0.0, 0.0).abs().mean()
+    else:
+        def step():
+            return train_step(model, criterion, optimizer, samples, targets, captions, cats)
+
     if a.graphs:
-        if world > 1:
-            raise SystemExit("--graphs is single-GPU for now")
+        if world > 1 or a.forward_only:
+            raise SystemExit("--graphs is single-GPU train-step only")
+        print("warning: --graphs is experimental (DESIGN.md section 7)", file=sys.stderr, flush=True)
         from gdino_amd import graphs
         text, _ = model.prepare_text(captions, device)
         graphs.capture(model, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
@@ -203,7 +246,7 @@ def main(argv=None, device_type="cuda"):
         sync()
 
     for _ in range(a.warmup):
-        train_step(model, criterion, optimizer, samples, targets, captions, cats)
+        step()
     sync()
     if world > 1:
         dist.barrier()
@@ -214,7 +257,7 @@ def main(argv=None, device_type="cuda"):
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = train_step(model, criterion, optimizer, samples, targets, captions, cats)
+        loss = step()
     sync()
     if world > 1:
         dist.barrier()
@@ -230,11 +273,14 @@ def main(argv=None, device_type="cuda"):
     # one extra step, outside the timed region, with HIP events around every
     # C-ABI call: device time per HIP entry point (all kernel families, not
     # only the MSDA launches the roofline prices)
+    # (single GPU only: under DDP a rank that failed here would leave the
+    # others blocked in the gradient all-reduce, and the extra step would
+    # also move the weights)
     hip_calls = None
-    if on_gpu:
+    if on_gpu and world == 1:
         _lib.call_timer = _lib.CallTimer()
         try:
-            train_step(model, criterion, optimizer, samples, targets, captions, cats)
+            step()
             hip_calls = _lib.call_timer.summary()
         except Exception as e:  # diagnostics only: never cost the bench line
             hip_calls = {"error": repr(e)[:300]}
@@ -259,8 +305,10 @@ def main(argv=None, device_type="cuda"):
                for (k, lq), d in sorted(kern.items())}
 
     if rank == 0:
+        mode = "forward (eval, no autograd)" if a.forward_only else "train step (fwd+bwd+AdamW)"
         res = {
-            "metric": "train images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU",
+            "metric": ("forward images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU" if a.forward_only else
+                       "train images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU"),
             "value": value,
             "unit": "images/s",
             "n_gpus": world,
@@ -272,7 +320,7 @@ def main(argv=None, device_type="cuda"):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (odvg-shaped batch, random weights, 256-token captions, 8 boxes/image)",
-            "config": {"workload": f"GroundingDINO-{a.backbone} + BERT-base train step (fwd+bwd+AdamW), "
+            "config": {"workload": f"GroundingDINO-{a.backbone} + BERT-base {mode}, "
                                    f"{a.height}x{a.width}, 900 queries, 4 levels",
                        "global_batch": a.bs * world, "per_gpu_batch": a.bs, "image": [a.height, a.width],
                        "text_tokens": 256, "parallelism": f"dp{world}"},
@@ -286,11 +334,15 @@ def main(argv=None, device_type="cuda"):
                         "msda_bwd": os.environ.get("GD_MSDA_BWD", "auto")},
             "loss": loss_v,
         }
+        if not math.isfinite(loss_v):
+            res["error"] = f"non-finite loss {loss_v}: the step diverged, the throughput is not a valid measurement"
         if not a.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(a.bs)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not math.isfinite(loss_v):
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

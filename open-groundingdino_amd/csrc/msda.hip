@@ -56,20 +56,27 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 //           (msda_bwd_tiled; 3.77 ms vs lane32's 2.19 ms on the box);
 //   enc     2-D query tiles per level, vector lanes, packed LDS boxes
 //           (msda_bwd_enc, msda_enc.inc);
-//   auto / unset: see bwd_variant().
+//   auto / unset: enc when the host passes the level shapes (the model's
+//           encoder does), else lane32.  Measured at 800x1333 bs=2: enc
+//           0.82 ms on the reference-init geometry the bench runs at and
+//           1.90 ms on a 2-px random spread, lane32 2.19 / 2.09 ms.
 enum class BwdVariant { kLane32, kTiled, kEnc };
 inline BwdVariant bwd_variant() {
   const char* e = getenv("GD_MSDA_BWD");
   if (e && strcmp(e, "tiled") == 0) return BwdVariant::kTiled;
-  if (e && strcmp(e, "enc") == 0) return BwdVariant::kEnc;
-  return BwdVariant::kLane32;
+  if (e && strcmp(e, "lane32") == 0) return BwdVariant::kLane32;
+  return BwdVariant::kEnc;  // "enc", "auto", unset: msda_bwd_enc when the level shapes are known
 }
 
 // msda_bwd_enc geometry (tuning overrides, default below):
 //   GD_MSDA_ENC_TILE="THxTW,THxTW,THxTW,THxTW"  query tile extents per query level
 //   GD_MSDA_ENC_CAP="r0,r1,r2,r3"               LDS rows of each sampled level's box
 inline void enc_geometry(int (&th)[4], int (&tw)[4], int (&cap)[4]) {
-  static const int dth[4] = {8, 8, 4, 4}, dtw[4] = {16, 8, 8, 8}, dcap[4] = {224, 96, 64, 64};
+  // 4 x 4 query tiles on every level and 64 / 40 / 24 / 28 box rows (+ one
+  // spare row each: 160 rows, 20 KB of LDS per 2-wave workgroup, so the
+  // 122-VGPR waves, not LDS, limit occupancy): the fastest of the tilings
+  // measured by tools/msda_microbench.py --enc-variants
+  static const int dth[4] = {4, 4, 4, 4}, dtw[4] = {4, 4, 4, 4}, dcap[4] = {64, 40, 24, 28};
   for (int l = 0; l < 4; ++l) { th[l] = dth[l]; tw[l] = dtw[l]; cap[l] = dcap[l]; }
   if (const char* e = getenv("GD_MSDA_ENC_TILE")) {
     int v[8];
@@ -188,7 +195,7 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
   // backward with LDS pre-aggregation.  Cross-attention (the decoder's 900
   // score-sorted queries) keeps the direct-atomic kernel.
   const BwdVariant variant = bwd_variant();
-  if ((dt == GD_F32 || dt == GD_BF16) && lane_ok && Lq == S && variant == BwdVariant::kEnc && shapes_host &&
+  if ((dt == GD_F32 || dt == GD_BF16) && lane_ok && Lq == S && M == 8 && variant == BwdVariant::kEnc && shapes_host &&
       aligned16(value) && aligned16(grad_out) && aligned16(attn) && aligned16(grad_attn)) {
     EncTiles tl{};
     int th[4], tw[4], cap[4];
@@ -207,7 +214,7 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
       nt += ((h + th[l] - 1) / th[l]) * tl.tx[l];
       tl.rbase[l] = rows;
       tl.rcap[l] = cap[l];
-      rows += cap[l];
+      rows += cap[l] + 1;  // + the region's spare row
     }
     tl.tstart[4] = int(nt);
     const int64_t blocks = int64_t(N) * nt * M;

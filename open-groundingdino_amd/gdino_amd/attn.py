@@ -118,6 +118,11 @@ def attention_hip(q, k, v, attn_mask=None, scale=None, dropout_p=0.0):
         return F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=dropout_p, scale=scale)
     scale = q.shape[-1] ** -0.5 if scale is None else scale
     if dropout_p > 0.0:
+        if q.is_cuda and torch.cuda.is_current_stream_capturing():
+            # a host-drawn seed would be baked into a captured HIP graph and
+            # every replay would apply the same mask: use PyTorch's dropout,
+            # whose Philox offset is graph-safe
+            return F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=dropout_p, scale=scale)
         # per-call mask seed from torch's (CPU) generator: torch.manual_seed
         # reproduces it, no device sync
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())

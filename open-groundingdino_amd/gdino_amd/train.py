@@ -154,6 +154,14 @@ def train_step(model, criterion, optimizer, samples, targets, captions, cat_list
     return loss.detach()
 
 
+def forward_step(model, samples, captions, amp_dtype=torch.bfloat16):
+    """BASELINE config 2: one inference forward (eval mode, no autograd) of
+    model(samples, captions=...) under bf16 autocast; returns the output dict."""
+    dev_type = samples.tensors.device.type
+    with torch.no_grad(), torch.autocast(device_type=dev_type, dtype=amp_dtype, enabled=amp_dtype is not None):
+        return model(samples, captions=captions)
+
+
 def build_training(args, device):
     from models.GroundingDINO import build_groundingdino
     model, criterion, post = build_groundingdino(args)

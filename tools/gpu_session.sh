@@ -54,8 +54,10 @@ core)
       > gpurun_out/s_gpu_tests.log 2>&1 &&
   step "bench (default)" &&
   T 600 python3 bench.py > gpurun_out/s_bench.log 2>&1 &&
-  step "bench (tiled encoder backward)" &&
-  GD_MSDA_BWD=tiled T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_bench_tiled.log 2>&1 &&
+  step "bench (lane32 encoder backward, A/B)" &&
+  GD_MSDA_BWD=lane32 T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_bench_lane32.log 2>&1 &&
+  step "bench (forward only, config 2)" &&
+  T 600 python3 bench.py --no-cpu-baseline --forward-only > gpurun_out/s_bench_fwd.log 2>&1 &&
   prof_trace s_prof --steps 3 --warmup 2 &&
   prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&
   prof_pmc s_pmc_write WRITE_SIZE --steps 1 --warmup 1 &&

@@ -93,14 +93,14 @@ ENC_VARIANTS = [
     ("enc 8x16 r256", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x16,8x8,4x8,4x8",
                        "GD_MSDA_ENC_CAP": "160,48,24,24"}),
     ("enc 4x8 r256", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "96,64,48,48"}),
-    ("enc 4x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "80,32,24,24"}),
+    ("enc 4x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "76,32,24,24"}),
     ("enc 4x16 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x16,4x8,4x4,4x4",
-                       "GD_MSDA_ENC_CAP": "96,32,16,16"}),
-    ("enc 8x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "96,32,16,16"}),
-    ("enc 4x8 r256 dsadd", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4",
-                            "GD_MSDA_ENC_CAP": "96,64,48,48", "GD_MSDA_ENC_MODE": "1"}),
-    ("enc 8x16 r256 dsadd", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x16,8x8,4x8,4x8",
-                             "GD_MSDA_ENC_CAP": "160,48,24,24", "GD_MSDA_ENC_MODE": "1"}),
+                       "GD_MSDA_ENC_CAP": "92,32,16,16"}),
+    ("enc 8x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x8,4x8,4x4,4x4", "GD_MSDA_ENC_CAP": "92,32,16,16"}),
+    ("enc 4x4 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x4,4x4,4x4,4x4", "GD_MSDA_ENC_CAP": "64,40,24,28"}),
+    ("enc 4x8 r160 rmax4", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x4,4x4",
+                            "GD_MSDA_ENC_CAP": "76,32,24,24", "GD_MSDA_ENC_RMAX": "4"}),
+    ("enc 2x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "2x8,2x8,2x4,2x4", "GD_MSDA_ENC_CAP": "60,40,28,28"}),
 ]
 ENC_PROBES = []
 
