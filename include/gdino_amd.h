@@ -311,6 +311,8 @@ gd_status gd_contrastive_forward(gd_dtype dtype, const void* x, const int64_t* x
  * bytes of device memory.  Deterministic (fixed-order reduction).
  */
 int gd_wgrad_splits(int T, int O, int I);
+/* the same policy for `batch` independent products (gd_wgrad_batched) */
+int gd_wgrad_splits_batched(int T, int O, int I, int batch);
 /* Batched form: out[b] = grad_y[b]^T x[b] for b < batch (batch strides in
  * elements), written in out_dtype (F32 or BF16) with batch stride
  * batch_stride_out; grad_b only for batch == 1.  Used for the

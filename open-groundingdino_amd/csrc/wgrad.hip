@@ -31,19 +31,12 @@ __device__ __forceinline__ void st4(uint16_t* p, float4 v) {
 
 template <typename T> __device__ __forceinline__ float to_float(T v);
 template <> __device__ __forceinline__ float to_float<float>(float v) { return v; }
-template <> __device__ __forceinline__ float to_float<uint16_t>(uint16_t v) { return bf16_to_f32(v); }
 
 constexpr int kWgChunk = 32;             // tokens per staged chunk
 constexpr int kWgRow = kWgChunk + 8;     // LDS row pitch (elements): 16-B aligned rows
 
 template <typename T>
 __device__ __forceinline__ WFrag<T> lds_row8(const T* p);
-template <>
-__device__ __forceinline__ WFrag<uint16_t> lds_row8<uint16_t>(const uint16_t* p) {
-  WFrag<uint16_t> f;
-  f.v = *reinterpret_cast<const gd_bf16x8*>(p);
-  return f;
-}
 template <>
 __device__ __forceinline__ WFrag<float> lds_row8<float>(const float* p) {
   WFrag<float> f;
@@ -135,6 +128,153 @@ wgrad_kernel(const T* __restrict__ dy, int64_t ldy, int64_t bsy, const T* __rest
   if (do_bias && threadIdx.x < 64) part_b[part * O + o0 + threadIdx.x] = bsum;
 }
 
+// ---------------------------------------------------------------------------
+// bf16, any O, I multiple of 16: 128 x 128 output tile per workgroup (each
+// wave a 64 x 64 quarter: 4 x 4 MFMA 16x16x32 tiles, 64 accumulators), token
+// chunks of 32 staged ROW-major (16-B global loads, one ds_write_b128 each)
+// into a double-buffered LDS image and read TRANSPOSED into the MFMA operand
+// layout with ds_read_b64_tr_b16 (cdna_hip_programming.md T10): lane c of
+// 16-lane group g gets tokens 8g..8g+3 (+4) of feature c -- the k-slots of
+// the A (dY^T) and B (X) operands.  One barrier per chunk; the next chunk's
+// global loads are in flight during the current chunk's MFMAs.
+// LDS image of a [32 token][128 feature] chunk: 256-B rows, 16-B chunk ch of
+// row r at chunk ch ^ swz(r): a half-wave's transposed read (rows 8g+q and
+// 8g+8+q, one 32-B column pair) then covers 8 distinct pairs = all 64 banks,
+// and 8 consecutive lanes' ds_write_b128 (one row, chunks 0-7) 32 banks.
+constexpr int kTrChunk = 32;
+constexpr int kTrTile = 128;
+
+__device__ __forceinline__ int tr_elem(int r, int ch) {  // element offset of (row r, 16-B chunk ch)
+  return r * kTrTile + ((ch ^ (2 * (r & 3) + 8 * ((r >> 3) & 1))) << 3);
+}
+
+typedef short gd_i16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ gd_i16x4 lds_tr16(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) gd_i16x4*)(p));
+}
+
+// operand fragment (8 tokens 8g..8g+7 of feature fbase + c) from an image
+__device__ __forceinline__ WFrag<uint16_t> tr_frag(const uint16_t* img, int fbase, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int ch = (fbase >> 3) + (p >> 1), sub = 4 * (p & 1);
+  const gd_i16x4 lo = lds_tr16(img + tr_elem(8 * g + q, ch) + sub);
+  const gd_i16x4 hi = lds_tr16(img + tr_elem(8 * g + 4 + q, ch) + sub);
+  WFrag<uint16_t> f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint16_t l16 = uint16_t(lo[j]), h16 = uint16_t(hi[j]);
+    f.v[j] = __builtin_bit_cast(__bf16, l16);
+    f.v[4 + j] = __builtin_bit_cast(__bf16, h16);
+  }
+  return f;
+}
+
+// grid (ceil(I/128), ceil(O/128), batch * splits); batch b reads dy + b*bsy, x + b*bsx
+template <bool BIAS>
+__global__ void __launch_bounds__(256)
+wgrad_tr_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, const uint16_t* __restrict__ x,
+                int64_t ldx, int64_t bsx, int T_, int O, int I, int splits, int tokens_per_split,
+                float* __restrict__ part_w, float* __restrict__ part_b) {
+  __shared__ __attribute__((aligned(16))) uint16_t ys[2][kTrChunk * kTrTile];
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][kTrChunk * kTrTile];
+  __shared__ float bsum_s[BIAS ? 16 : 1][kTrTile];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int wo = wave >> 1, wi = wave & 1;  // the wave's 64 x 64 quarter
+  const int i0 = blockIdx.x * kTrTile, o0 = blockIdx.y * kTrTile;
+  const int bz = blockIdx.z / splits, split = blockIdx.z - bz * splits;
+  dy += bz * bsy;
+  x += bz * bsx;
+  const int64_t part = int64_t(bz) * splits + split;
+  const int tb = split * tokens_per_split;
+  const int te = min(T_, tb + tokens_per_split);
+  const bool do_bias = BIAS && blockIdx.x == 0;
+
+  // loader: vectors v = tid and tid + 256 of the chunk's 32 rows x 16 chunks
+  const int lrow = tid >> 4, lch = tid & 15;
+  const bool yok = o0 + 8 * lch < O, xok = i0 + 8 * lch < I;
+  const uint16_t* yp = dy + o0 + 8 * lch;
+  const uint16_t* xp = x + i0 + 8 * lch;
+  uint4 ry[2], rx[2];
+  auto load = [&](int t0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = t0 + lrow + 16 * h;
+      const bool in = t < te;
+      ry[h] = (in && yok) ? *reinterpret_cast<const uint4*>(yp + int64_t(t) * ldy) : make_uint4(0u, 0u, 0u, 0u);
+      rx[h] = (in && xok) ? *reinterpret_cast<const uint4*>(xp + int64_t(t) * ldx) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  float bacc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bacc[e] = 0.f;
+
+  gd_f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+
+  if (tb < te) load(tb);
+  int buf = 0;
+  for (int t0 = tb; t0 < te; t0 += kTrChunk, buf ^= 1) {
+    uint16_t* yb = ys[buf];
+    uint16_t* xb = xs[buf];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<uint4*>(yb + tr_elem(lrow + 16 * h, lch)) = ry[h];
+      *reinterpret_cast<uint4*>(xb + tr_elem(lrow + 16 * h, lch)) = rx[h];
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bacc[0] += bf16_lo(ry[h].x); bacc[1] += bf16_hi(ry[h].x);
+        bacc[2] += bf16_lo(ry[h].y); bacc[3] += bf16_hi(ry[h].y);
+        bacc[4] += bf16_lo(ry[h].z); bacc[5] += bf16_hi(ry[h].z);
+        bacc[6] += bf16_lo(ry[h].w); bacc[7] += bf16_hi(ry[h].w);
+      }
+    }
+    if (t0 + kTrChunk < te) load(t0 + kTrChunk);  // next chunk in flight during the MFMAs
+    __syncthreads();  // image `buf` complete (and `buf ^ 1` consumed one iteration ago)
+    WFrag<uint16_t> af[4], bfr[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) af[m] = tr_frag(yb, 64 * wo + 16 * m, lane);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(xb, 64 * wi + 16 * n, lane);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = wmma(af[m], bfr[n], acc[m][n]);
+  }
+  // partial tile: (o0 + 64wo + 16m + 4g + r, i0 + 64wi + 16n + c)
+  float* pw = part_w + part * O * I;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = o0 + 64 * wo + 16 * m + 4 * g + r;
+      if (o < O) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int i = i0 + 64 * wi + 16 * n + c;
+          if (i < I) pw[int64_t(o) * I + i] = acc[m][n][r];
+        }
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum_s[lrow][8 * lch + e] = bacc[e];
+    __syncthreads();
+    if (tid < kTrTile && o0 + tid < O) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sum += bsum_s[k][tid];
+      part_b[part * O + o0 + tid] = sum;
+    }
+  }
+}
+
 // out[b] = sum over splits of the partials (4 columns per thread), written in
 // fp32 or bf16 with batch stride ob; db (batch 1) likewise
 template <typename TO>
@@ -174,13 +314,17 @@ extern "C" size_t gd_wgrad_workspace_bytes(int O, int I, int splits) {
   return sizeof(float) * (size_t(splits) * O * I + size_t(splits) * O);
 }
 
-extern "C" int gd_wgrad_splits(int T, int O, int I) {
-  // about 1024 workgroups, at least 256 tokens each
-  const int tiles = (O / 64) * (I / 64);
-  int s = tiles > 0 ? (1024 + tiles - 1) / tiles : 1;
-  const int cap = T / 256 > 1 ? T / 256 : 1;
+extern "C" int gd_wgrad_splits_batched(int T, int O, int I, int batch) {
+  // about 384 workgroups of 128 x 128 output tiles (1.5 per CU), at least
+  // 128 tokens each: the fp32 partials (splits x O x I) stay a fraction of
+  // the token-major inputs the kernel streams
+  const int tiles = ((O + kTrTile - 1) / kTrTile) * ((I + kTrTile - 1) / kTrTile) * (batch > 0 ? batch : 1);
+  int s = tiles > 0 ? (384 + tiles - 1) / tiles : 1;
+  const int cap = T / 128 > 1 ? T / 128 : 1;
   return s < 1 ? 1 : (s > cap ? cap : s);
 }
+
+extern "C" int gd_wgrad_splits(int T, int O, int I) { return gd_wgrad_splits_batched(T, O, I, 1); }
 
 extern "C" gd_status gd_wgrad_batched(gd_dtype dt, const void* grad_y, int64_t ldy, int64_t batch_stride_y,
                                       const void* x, int64_t ldx, int64_t batch_stride_x, int T, int O, int I,
@@ -188,9 +332,12 @@ extern "C" gd_status gd_wgrad_batched(gd_dtype dt, const void* grad_y, int64_t l
                                       int64_t batch_stride_out, float* grad_b, gd_stream_t stream) {
   GD_REQUIRE(dt == GD_F32 || dt == GD_BF16, "wgrad: dtype %d not supported (F32, BF16)", int(dt));
   GD_REQUIRE(out_dtype == GD_F32 || out_dtype == GD_BF16, "wgrad: out dtype %d not supported", int(out_dtype));
-  GD_REQUIRE(T >= 0 && O > 0 && I > 0 && O % 64 == 0 && I % 64 == 0 && splits >= 1 && batch >= 1 &&
+  // bf16: O, I multiples of 16 (the 128 x 128 transposed-read kernel);
+  // fp32: multiples of 64 (the 64 x 64 kernel)
+  const int gran = dt == GD_BF16 ? 16 : 64;
+  GD_REQUIRE(T >= 0 && O > 0 && I > 0 && O % gran == 0 && I % gran == 0 && splits >= 1 && batch >= 1 &&
                  int64_t(batch) * splits < 65536 && O / 64 < 65536,
-             "wgrad: bad sizes T=%d O=%d I=%d (multiples of 64) batch=%d splits=%d", T, O, I, batch, splits);
+             "wgrad: bad sizes T=%d O=%d I=%d (multiples of %d) batch=%d splits=%d", T, O, I, gran, batch, splits);
   GD_REQUIRE(!grad_b || batch == 1, "wgrad: bias gradient only for batch 1");
   GD_REQUIRE(grad_y && x && workspace && out, "wgrad: null pointer");
   const int64_t align = 16 / (dt == GD_BF16 ? 2 : 4);
@@ -204,15 +351,23 @@ extern "C" gd_status gd_wgrad_batched(gd_dtype dt, const void* grad_y, int64_t l
   float* part_w = static_cast<float*>(workspace);
   float* part_b = part_w + int64_t(batch) * splits * O * I;
   const int tps = ((T + splits - 1) / splits + kWgChunk - 1) / kWgChunk * kWgChunk;
-  const dim3 grid(unsigned(I / 64), unsigned(O / 64), unsigned(batch * splits));
-  if (dt == GD_BF16)
-    hipLaunchKernelGGL((wgrad_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy, batch_stride_y,
-                       (const uint16_t*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
-                       grad_b ? part_b : nullptr);
-  else
+  if (dt == GD_BF16) {
+    const dim3 grid(unsigned((I + kTrTile - 1) / kTrTile), unsigned((O + kTrTile - 1) / kTrTile),
+                    unsigned(batch * splits));
+    if (grad_b)
+      hipLaunchKernelGGL((wgrad_tr_kernel<true>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy,
+                         batch_stride_y, (const uint16_t*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
+                         part_b);
+    else
+      hipLaunchKernelGGL((wgrad_tr_kernel<false>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy,
+                         batch_stride_y, (const uint16_t*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
+                         nullptr);
+  } else {
+    const dim3 grid(unsigned(I / 64), unsigned(O / 64), unsigned(batch * splits));
     hipLaunchKernelGGL((wgrad_kernel<float>), grid, dim3(256), 0, s, (const float*)grad_y, ldy, batch_stride_y,
                        (const float*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
                        grad_b ? part_b : nullptr);
+  }
   GD_LAUNCH_CHECK("wgrad");
   const int64_t n = int64_t(O) * I / 4 * batch + (grad_b ? O : 0);
   const dim3 rg(unsigned((n + 255) / 256));

@@ -90,7 +90,7 @@ def _token_linear_ok(x, params, out_features, dt) -> bool:
     if any(p.dtype != torch.float32 or not p.requires_grad for p in params):
         return False
     from . import wgrad
-    return wgrad.eligible(x, out_features)
+    return wgrad.eligible(x, out_features, dt)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:

@@ -248,6 +248,24 @@ inline void wave_gather(const void* mine, size_t nbytes, void* all) {
   }
 }
 
+// ds_read_b64_tr_b16 (gfx950): per 16-lane group, lane 4q+p supplies the
+// address of row q, columns 4p..4p+3 of a 4 x 16 block of 16-bit elements;
+// lane i receives column i of the 4 rows (row q in element q)
+typedef short gd_emu_i16x4 __attribute__((ext_vector_type(4)));
+inline gd_emu_i16x4 ds_read_tr16_b64(const void* p) {
+  const uint64_t mine = uint64_t(uintptr_t(p));
+  uint64_t all[64];
+  wave_gather(&mine, sizeof(mine), all);
+  const unsigned lane = lane_id(), base = lane & ~15u, i = lane & 15u;
+  gd_emu_i16x4 r;
+  for (unsigned q = 0; q < 4; ++q) {
+    const int16_t* a = reinterpret_cast<const int16_t*>(uintptr_t(all[base + 4 * q + i / 4]));
+    r[q] = a[i % 4];
+  }
+  return r;
+}
+
+
 inline float bf16_bits_to_f(uint16_t h) {
   uint32_t u = uint32_t(h) << 16;
   float f;
@@ -313,6 +331,7 @@ void launch(dim3 g, dim3 b, F&& f) {
 #define __syncthreads() ::gd_emu::syncthreads()
 #define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
 #define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
+#define __builtin_amdgcn_ds_read_tr16_b64_v4i16(p) ::gd_emu::ds_read_tr16_b64((const void*)(uintptr_t)(p))
 #define __builtin_amdgcn_ds_swizzle(v, pattern) ::gd_emu::ds_swizzle((v), (pattern))
 #define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) \
   ::gd_emu::update_dpp((old), (src), (ctrl), (rm), (bm), (bc))

@@ -583,6 +583,9 @@ def test_emulated_msda_prologue(ref_dim, dtype):
     (777, 64, 192, 3, torch.float32, 1e-6),       # splits not dividing T, 3 column tiles
     (300, 192, 128, 1, torch.bfloat16, 1e-6),     # bf16-exact inputs, fp32 accumulation
     (64, 64, 64, 5, torch.float32, 1e-6),         # more splits than token chunks: empty splits
+    (333, 48, 80, 2, torch.bfloat16, 1e-6),       # bf16 128-tile kernel: O, I multiples of 16, partial tiles
+    (700, 384, 256, 3, torch.bfloat16, 1e-6),     # bf16: 3 x 2 tiles, token tail
+    (96, 16, 16, 7, torch.bfloat16, 1e-6),        # bf16: empty splits, one 16-wide column
 ])
 def test_emulated_wgrad(T, O, I, splits, dtype, tol):
     g = torch.Generator().manual_seed(T + O)
