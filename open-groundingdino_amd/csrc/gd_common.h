@@ -54,6 +54,15 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+// Bijective XCD-contiguous remap: hardware deals blocks b, b+8, b+16, ... to
+// one XCD; give that XCD a contiguous chunk of the logical grid instead.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7;
+  const int xcd = b & 7, local = b >> 3;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + local;
+}
+
 // ---- DPP lane exchange inside 8/16-lane groups ----------------------------
 // quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), row_half_mirror (i <-> 7-i),
 // row_ror:8 (i <-> i^8 inside a 16-lane row).

@@ -15,51 +15,151 @@
 // Device code and its design notes: wattn_kernels.inc.
 #include "gd_common.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace gd {
 namespace {
 #include "wattn_kernels.inc"
 
-constexpr int kWpw = 4;  // backward: windows per wave (one head per block)
+constexpr int kMaxTokens = 144;  // 12x12 windows (Swin-B/L at 384)
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+int isqrt_exact(int n) {  // ws with ws*ws == n, else 0
+  for (int w = 1; w * w <= n; ++w)
+    if (w * w == n) return w;
+  return 0;
+}
+
 gd_status check(gd_dtype dt, const void* qkv, const float* table, const int64_t* ridx, int B_, int N, int nH,
-                int hd, int nW) {
+                int hd, int nW, int ws) {
   GD_REQUIRE(dt == GD_F32 || dt == GD_BF16, "window_attn: dtype %d not supported (F32, BF16)", int(dt));
-  GD_REQUIRE(B_ >= 0 && N > 0 && N <= kWTok && nH > 0 && nW > 0,
-             "window_attn: bad sizes B_=%d N=%d (1..%d) nH=%d nW=%d", B_, N, kWTok, nH, nW);
+  GD_REQUIRE(B_ >= 0 && N > 0 && N <= kMaxTokens && nH > 0 && nW > 0,
+             "window_attn: bad sizes B_=%d N=%d (1..%d) nH=%d nW=%d", B_, N, kMaxTokens, nH, nW);
   GD_REQUIRE(hd == 32, "window_attn: head_dim %d not supported (32: Swin-T/S/B/L)", hd);
   GD_REQUIRE(B_ % nW == 0, "window_attn: B_=%d is not a multiple of nW=%d", B_, nW);
+  GD_REQUIRE(ridx || (ws > 0 && ws * ws == N && ws <= 12),
+             "window_attn: rel_index NULL needs a square window of <= 12x12 tokens (N=%d)", N);
   GD_REQUIRE(int64_t(B_) * N * 3 * nH * hd < (int64_t(1) << 31), "window_attn: qkv too large for int32 offsets");
-  GD_REQUIRE(B_ == 0 || (qkv && table && ridx), "window_attn: null pointer");
+  GD_REQUIRE(B_ == 0 || (qkv && table), "window_attn: null pointer");
   GD_REQUIRE(aligned16(qkv), "window_attn: qkv must be 16-byte aligned");
   return GD_OK;
 }
 
-template <typename T>
-void launch_fwd(const void* qkv, const void* padv, const WinGeo& geo, const float* table, const int64_t* ridx,
-                const float* mask, int B_, int N, int nH, int nW, float scale, void* out, float* lse, hipStream_t s) {
-  const dim3 grid(unsigned((B_ + 3) / 4), unsigned(nH));
-  hipLaunchKernelGGL((wattn_fwd_kernel<T, 32>), grid, dim3(256), 0, s, (const T*)qkv, (const T*)padv, geo, table,
-                     ridx, mask, B_, N, nH, nW, scale, (T*)out, lse);
+// windows per block: about 2048 blocks over the whole launch, at most 8
+int windows_per_block(int B_, int nH) {
+  const int64_t tasks = int64_t(B_) * nH;
+  return int(std::max<int64_t>(1, std::min<int64_t>(8, tasks / 2048)));
+}
+
+WinCtx make_ctx(const float* table, const int64_t* ridx, const float* mask, int N, int nH, int nW, int ws,
+                float scale) {
+  WinCtx X{};
+  X.table = table;
+  X.ridx = ridx;
+  X.mask = mask;
+  X.N = N;
+  X.nH = nH;
+  X.nW = nW;
+  X.h = 0;
+  X.c0 = ws > 0 ? (ws - 1) * (2 * ws - 1) + ws - 1 : 0;
+  X.scale = scale;
+  return X;
+}
+
+template <typename T, int NT, int MODE>
+void launch_fwd_nt(const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X, int B_, void* out,
+                   float* lse, hipStream_t s) {
+  const int wpb = windows_per_block(B_, X.nH);
+  const unsigned nblk = unsigned((B_ + wpb - 1) / wpb) * unsigned(X.nH);
+  hipLaunchKernelGGL((wattn_fwd_kernel<T, NT, MODE>), dim3(nblk), dim3(64 * NT), 0, s, (const T*)qkv, (const T*)padv,
+                     geo, X, B_, wpb, (T*)out, lse);
+}
+
+template <typename T, int NT>
+void launch_fwd_mode(int mode, const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X, int B_,
+                     void* out, float* lse, hipStream_t s) {
+  if (mode == kModeStd) {
+    launch_fwd_nt<T, NT, kModeStd>(qkv, padv, geo, X, B_, out, lse, s);
+  } else if (mode == kModeRegion) {
+    launch_fwd_nt<T, NT, kModeRegion>(qkv, padv, geo, X, B_, out, lse, s);
+  } else {
+    launch_fwd_nt<T, NT, kModeAny>(qkv, padv, geo, X, B_, out, lse, s);
+  }
 }
 
 template <typename T>
-void launch_bwd(const void* qkv, const void* padv, const WinGeo& geo, const float* table, const int64_t* ridx,
-                const float* mask, const void* out, const void* dout, const float* lse, int B_, int N, int nH,
-                int nW, float scale, void* dqkv, float* grad_pad, float* dtable, hipStream_t s) {
-  const dim3 grid(unsigned((B_ + 4 * kWpw - 1) / (4 * kWpw)), unsigned(nH));
-  hipLaunchKernelGGL((wattn_bwd_kernel<T, 32, kWpw>), grid, dim3(256), 0, s, (const T*)qkv, (const T*)padv, geo,
-                     table, ridx, mask, (const T*)out, (const T*)dout, lse, B_, N, nH, nW, scale, (T*)dqkv,
-                     grad_pad, dtable);
+void launch_fwd(int mode, const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X, int B_, void* out,
+                float* lse, hipStream_t s) {
+  if (X.N <= 64) {
+    launch_fwd_mode<T, 4>(mode, qkv, padv, geo, X, B_, out, lse, s);
+  } else {
+    launch_fwd_mode<T, 9>(mode, qkv, padv, geo, X, B_, out, lse, s);
+  }
+}
+
+// backward dS-over-windows sums for 7x7 windows: registers (default) or LDS
+// atomics per window (GD_WATTN_REGSUM=0)
+bool bwd_regsum() {
+  static const bool on = [] {
+    const char* e = std::getenv("GD_WATTN_REGSUM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <typename T, int NT, int MODE>
+void launch_bwd_nt(const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X, const void* out,
+                   const void* dout, const float* lse, int B_, void* dqkv, float* grad_pad, float* dtable,
+                   hipStream_t s) {
+  const int wpb = windows_per_block(B_, X.nH);
+  const unsigned nblk = unsigned((B_ + wpb - 1) / wpb) * unsigned(X.nH);
+  if constexpr (NT <= 4) {
+    if (bwd_regsum()) {
+      hipLaunchKernelGGL((wattn_bwd_kernel<T, NT, MODE, true>), dim3(nblk), dim3(64 * NT), 0, s, (const T*)qkv,
+                         (const T*)padv, geo, X, (const T*)out, (const T*)dout, lse, B_, wpb, (T*)dqkv, grad_pad,
+                         dtable);
+      return;
+    }
+  }
+  {
+    hipLaunchKernelGGL((wattn_bwd_kernel<T, NT, MODE, false>), dim3(nblk), dim3(64 * NT), 0, s, (const T*)qkv,
+                       (const T*)padv, geo, X, (const T*)out, (const T*)dout, lse, B_, wpb, (T*)dqkv, grad_pad,
+                       dtable);
+  }
+}
+
+template <typename T, int NT>
+void launch_bwd_mode(int mode, const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X,
+                     const void* out, const void* dout, const float* lse, int B_, void* dqkv, float* grad_pad,
+                     float* dtable, hipStream_t s) {
+  if (mode == kModeStd) {
+    launch_bwd_nt<T, NT, kModeStd>(qkv, padv, geo, X, out, dout, lse, B_, dqkv, grad_pad, dtable, s);
+  } else if (mode == kModeRegion) {
+    launch_bwd_nt<T, NT, kModeRegion>(qkv, padv, geo, X, out, dout, lse, B_, dqkv, grad_pad, dtable, s);
+  } else {
+    launch_bwd_nt<T, NT, kModeAny>(qkv, padv, geo, X, out, dout, lse, B_, dqkv, grad_pad, dtable, s);
+  }
+}
+
+template <typename T>
+void launch_bwd(int mode, const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X, const void* out,
+                const void* dout, const float* lse, int B_, void* dqkv, float* grad_pad, float* dtable,
+                hipStream_t s) {
+  if (X.N <= 64) {
+    launch_bwd_mode<T, 4>(mode, qkv, padv, geo, X, out, dout, lse, B_, dqkv, grad_pad, dtable, s);
+  } else {
+    launch_bwd_mode<T, 9>(mode, qkv, padv, geo, X, out, dout, lse, B_, dqkv, grad_pad, dtable, s);
+  }
 }
 
 // image geometry -> WinGeo + window count; validates the sizes
 gd_status image_geo(int B, int H, int W, int ws, int sh, WinGeo* geo, int* B_) {
   GD_REQUIRE(B >= 0 && H > 0 && W > 0, "window_attn_image: bad sizes B=%d H=%d W=%d", B, H, W);
-  GD_REQUIRE(ws > 0 && ws * ws <= kWTok, "window_attn_image: window %d not supported (ws*ws <= %d)", ws, kWTok);
+  GD_REQUIRE(ws > 0 && ws * ws <= kMaxTokens, "window_attn_image: window %d not supported (ws*ws <= %d)", ws,
+             kMaxTokens);
   GD_REQUIRE(sh >= 0 && sh < ws, "window_attn_image: shift %d not in [0, window %d)", sh, ws);
   GD_REQUIRE(int64_t(B) * H * W < (int64_t(1) << 31), "window_attn_image: too many tokens");
   geo->img = 1;
@@ -76,8 +176,17 @@ gd_status image_geo(int B, int H, int W, int ws, int sh, WinGeo* geo, int* B_) {
   return GD_OK;
 }
 
-WinGeo window_geo() {
+// kernel variant: a given rel_index or mask tensor is read as given; with
+// both NULL the index is computed, and in the image layout a shift > 0
+// computes the reference's region mask (window-major: no mask)
+int win_mode(const int64_t* ridx, const float* mask, bool region) {
+  if (ridx || mask) return kModeAny;
+  return region ? kModeRegion : kModeStd;
+}
+
+WinGeo window_geo(int N) {
   WinGeo g{};
+  g.ws = isqrt_exact(N);
   return g;
 }
 
@@ -90,15 +199,18 @@ extern "C" gd_status gd_window_attn_forward(gd_dtype dt, const void* qkv, const 
                                            const int64_t* rel_index, const float* mask, int B_, int N, int nH,
                                            int head_dim, int nW, float scale, void* out, float* lse,
                                            gd_stream_t stream) {
-  const gd_status st = check(dt, qkv, table, rel_index, B_, N, nH, head_dim, nW);
+  const WinGeo geo = window_geo(N);
+  const gd_status st = check(dt, qkv, table, rel_index, B_, N, nH, head_dim, nW, geo.ws);
   if (st != GD_OK) return st;
   if (B_ == 0) return GD_OK;
   GD_REQUIRE(out && lse, "window_attn_forward: null output");
+  GD_REQUIRE(aligned16(out), "window_attn_forward: out must be 16-byte aligned");
+  const WinCtx X = make_ctx(table, rel_index, mask, N, nH, nW, geo.ws, scale);
   hipStream_t s = as_hip(stream);
   if (dt == GD_BF16) {
-    launch_fwd<uint16_t>(qkv, nullptr, window_geo(), table, rel_index, mask, B_, N, nH, nW, scale, out, lse, s);
+    launch_fwd<uint16_t>(win_mode(rel_index, mask, false), qkv, nullptr, geo, X, B_, out, lse, s);
   } else {
-    launch_fwd<float>(qkv, nullptr, window_geo(), table, rel_index, mask, B_, N, nH, nW, scale, out, lse, s);
+    launch_fwd<float>(win_mode(rel_index, mask, false), qkv, nullptr, geo, X, B_, out, lse, s);
   }
   GD_LAUNCH_CHECK("wattn_fwd");
   return GD_OK;
@@ -109,19 +221,19 @@ extern "C" gd_status gd_window_attn_backward(gd_dtype dt, const void* qkv, const
                                             const void* grad_out, const float* lse, int B_, int N, int nH,
                                             int head_dim, int nW, float scale, void* grad_qkv,
                                             float* grad_table, gd_stream_t stream) {
-  const gd_status st = check(dt, qkv, table, rel_index, B_, N, nH, head_dim, nW);
+  const WinGeo geo = window_geo(N);
+  const gd_status st = check(dt, qkv, table, rel_index, B_, N, nH, head_dim, nW, geo.ws);
   if (st != GD_OK) return st;
   if (B_ == 0) return GD_OK;
   GD_REQUIRE(out && grad_out && lse && grad_qkv && grad_table, "window_attn_backward: null pointer");
   GD_REQUIRE(aligned16(out) && aligned16(grad_out) && aligned16(grad_qkv),
              "window_attn_backward: out / grad_out / grad_qkv must be 16-byte aligned");
+  const WinCtx X = make_ctx(table, rel_index, mask, N, nH, nW, geo.ws, scale);
   hipStream_t s = as_hip(stream);
   if (dt == GD_BF16) {
-    launch_bwd<uint16_t>(qkv, nullptr, window_geo(), table, rel_index, mask, out, grad_out, lse, B_, N, nH, nW,
-                         scale, grad_qkv, nullptr, grad_table, s);
+    launch_bwd<uint16_t>(win_mode(rel_index, mask, false), qkv, nullptr, geo, X, out, grad_out, lse, B_, grad_qkv, nullptr, grad_table, s);
   } else {
-    launch_bwd<float>(qkv, nullptr, window_geo(), table, rel_index, mask, out, grad_out, lse, B_, N, nH, nW,
-                      scale, grad_qkv, nullptr, grad_table, s);
+    launch_bwd<float>(win_mode(rel_index, mask, false), qkv, nullptr, geo, X, out, grad_out, lse, B_, grad_qkv, nullptr, grad_table, s);
   }
   GD_LAUNCH_CHECK("wattn_bwd");
   return GD_OK;
@@ -136,17 +248,18 @@ extern "C" gd_status gd_window_attn_image_forward(gd_dtype dt, const void* qkv, 
   int B_ = 0;
   gd_status st = image_geo(B, H, W, window, shift, &geo, &B_);
   if (st != GD_OK) return st;
-  st = check(dt, qkv, table, rel_index, B_, window * window, nH, head_dim, mask ? geo.nWi : 1);
+  const int N = window * window, nW = mask ? geo.nWi : 1;
+  st = check(dt, qkv, table, rel_index, B_, N, nH, head_dim, nW, window);
   if (st != GD_OK) return st;
   if (B_ == 0) return GD_OK;
   GD_REQUIRE(out && lse, "window_attn_image_forward: null output");
-  GD_REQUIRE(aligned16(qkv_bias), "window_attn_image_forward: qkv_bias must be 16-byte aligned");
+  GD_REQUIRE(aligned16(qkv_bias) && aligned16(out), "window_attn_image_forward: qkv_bias / out must be 16-byte aligned");
+  const WinCtx X = make_ctx(table, rel_index, mask, N, nH, nW, window, scale);
   hipStream_t s = as_hip(stream);
-  const int N = window * window, nW = mask ? geo.nWi : 1;
   if (dt == GD_BF16) {
-    launch_fwd<uint16_t>(qkv, qkv_bias, geo, table, rel_index, mask, B_, N, nH, nW, scale, out, lse, s);
+    launch_fwd<uint16_t>(win_mode(rel_index, mask, shift > 0), qkv, qkv_bias, geo, X, B_, out, lse, s);
   } else {
-    launch_fwd<float>(qkv, qkv_bias, geo, table, rel_index, mask, B_, N, nH, nW, scale, out, lse, s);
+    launch_fwd<float>(win_mode(rel_index, mask, shift > 0), qkv, qkv_bias, geo, X, B_, out, lse, s);
   }
   GD_LAUNCH_CHECK("wattn_image_fwd");
   return GD_OK;
@@ -162,20 +275,21 @@ extern "C" gd_status gd_window_attn_image_backward(gd_dtype dt, const void* qkv,
   int B_ = 0;
   gd_status st = image_geo(B, H, W, window, shift, &geo, &B_);
   if (st != GD_OK) return st;
-  st = check(dt, qkv, table, rel_index, B_, window * window, nH, head_dim, mask ? geo.nWi : 1);
+  const int N = window * window, nW = mask ? geo.nWi : 1;
+  st = check(dt, qkv, table, rel_index, B_, N, nH, head_dim, nW, window);
   if (st != GD_OK) return st;
   if (B_ == 0) return GD_OK;
   GD_REQUIRE(out && grad_out && lse && grad_qkv && grad_table, "window_attn_image_backward: null pointer");
   GD_REQUIRE(aligned16(out) && aligned16(grad_out) && aligned16(grad_qkv) && aligned16(qkv_bias),
              "window_attn_image_backward: out / grad_out / grad_qkv / qkv_bias must be 16-byte aligned");
+  const WinCtx X = make_ctx(table, rel_index, mask, N, nH, nW, window, scale);
   hipStream_t s = as_hip(stream);
-  const int N = window * window, nW = mask ? geo.nWi : 1;
   if (dt == GD_BF16) {
-    launch_bwd<uint16_t>(qkv, qkv_bias, geo, table, rel_index, mask, out, grad_out, lse, B_, N, nH, nW, scale,
-                         grad_qkv, qkv_bias ? grad_qkv_bias : nullptr, grad_table, s);
+    launch_bwd<uint16_t>(win_mode(rel_index, mask, shift > 0), qkv, qkv_bias, geo, X, out, grad_out, lse, B_, grad_qkv, qkv_bias ? grad_qkv_bias : nullptr,
+                         grad_table, s);
   } else {
-    launch_bwd<float>(qkv, qkv_bias, geo, table, rel_index, mask, out, grad_out, lse, B_, N, nH, nW, scale,
-                      grad_qkv, qkv_bias ? grad_qkv_bias : nullptr, grad_table, s);
+    launch_bwd<float>(win_mode(rel_index, mask, shift > 0), qkv, qkv_bias, geo, X, out, grad_out, lse, B_, grad_qkv, qkv_bias ? grad_qkv_bias : nullptr,
+                      grad_table, s);
   }
   GD_LAUNCH_CHECK("wattn_image_bwd");
   return GD_OK;

@@ -5,6 +5,11 @@ eager-PyTorch fallback behind it: if the library is missing, or a tensor is
 not on a ROCm device, the call raises — mirroring the reference extension,
 whose CPU backend raises "Not implemented on the CPU"
 (models/GroundingDINO/ops/src/ms_deform_attn.h:38,60).
+
+The one exception is the op the reference dispatches by device: MSDA on
+HOST tensors runs libgdino_cpu.so (csrc/cpu/msda_cpu.cpp), a C++/OpenMP
+implementation exported under the same C-ABI with a NULL stream, where the
+reference has its AT_ERROR stub.  Device tensors never reach it.
 """
 from __future__ import annotations
 
@@ -139,6 +144,43 @@ class CallTimer:
 call_timer = None  # set to a CallTimer to time every entry point
 MFMA_BF16_PEAK = 2.5e15  # FLOP/s, dense bf16 (MI355X_MICROARCH.md chip table)
 HBM_PEAK = 8.0e12  # B/s, same table
+
+
+CPU_LIB_PATH = os.environ.get("GDINO_CPU_LIB", os.path.join(_HERE, "lib", "libgdino_cpu.so"))
+_cpu_lib = None
+
+
+def cpu_lib() -> ctypes.CDLL:
+    """Load (once) the CPU backend of the MSDA op (same C-ABI, host pointers,
+    NULL stream); raise if it is not built."""
+    global _cpu_lib
+    if _cpu_lib is not None:
+        return _cpu_lib
+    with _lock:
+        if _cpu_lib is None:
+            if not os.path.exists(CPU_LIB_PATH):
+                raise RuntimeError(f"gdino_amd: CPU backend not found at {CPU_LIB_PATH}; build it with "
+                                   "make -C open-groundingdino_amd/csrc")
+            handle = ctypes.CDLL(CPU_LIB_PATH, mode=ctypes.RTLD_LOCAL)
+            for name, argtypes in _SIGNATURES.items():
+                if name.startswith("gd_msda_"):
+                    fn = getattr(handle, name)
+                    fn.argtypes = argtypes
+                    fn.restype = ctypes.c_int
+            handle.gd_last_error.restype = ctypes.c_char_p
+            handle.gd_runtime_info.restype = ctypes.c_char_p
+            if handle.gd_abi_version() != 1:
+                raise RuntimeError("gdino_amd: CPU backend ABI version mismatch")
+            _cpu_lib = handle
+    return _cpu_lib
+
+
+def call_cpu(name: str, *args) -> None:
+    """Run MSDA entry point ``name`` of the CPU backend (stream argument NULL)."""
+    status = getattr(cpu_lib(), name)(*args)
+    if status != GD_OK:
+        msg = cpu_lib().gd_last_error().decode(errors="replace")
+        raise GdError(f"{name} (CPU backend): status {status}: {msg}")
 
 
 def call(name: str, *args, flops: float | None = None, nbytes: float | None = None) -> None:

@@ -7,6 +7,10 @@ Contract kept from ops/src/cuda/ms_deform_attn_cuda.cu:20-153:
   * ``batch % min(batch, im2col_step) == 0`` else RuntimeError;
   * outputs are freshly allocated and owned by the caller;
   * work is enqueued on the current stream.
+Device dispatch as the reference's ops/src/ms_deform_attn.h:20-61: device
+tensors run the gfx950 kernels, HOST tensors the C++ CPU backend
+(libgdino_cpu.so, same C-ABI, NULL stream) where the reference raises "Not
+implemented on the CPU"; mixing devices raises.
 Differences (documented in DESIGN.md): the whole batch is one launch (no
 im2col_step chunking — it only bounded the reference's column buffer), bf16
 ``value`` is accepted (fp32 accumulate; sampling locations / weights stay
@@ -66,9 +70,19 @@ def _acc_dtype(value: torch.Tensor) -> torch.dtype:
     return torch.float64 if value.dtype == torch.float64 else torch.float32
 
 
+def _on_host(*tensors) -> bool:
+    """True when every tensor is a host tensor (the CPU backend), False when
+    every one is on the ROCm device; raise on a mix."""
+    devs = {t.is_cuda for t in tensors if t is not None}
+    if len(devs) > 1:
+        raise RuntimeError("ms_deform_attn: tensors must all be on the same device (host or ROCm)")
+    return devs == {False}
+
+
 def _check(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, im2col_step, extra=()):
-    _lib.require_device(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, *extra,
-                        what="ms_deform_attn")
+    if not _on_host(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, *extra):
+        _lib.require_device(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, *extra,
+                            what="ms_deform_attn")
     _lib.require_contiguous("ms_deform_attn", value=value, spatial_shapes=spatial_shapes,
                             level_start_index=level_start_index, sampling_loc=sampling_loc,
                             attn_weight=attn_weight)
@@ -102,6 +116,11 @@ def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_lo
     (N, S, M, D, L, Lq, P), loc, attn = _check(value, spatial_shapes, level_start_index,
                                                sampling_loc, attn_weight, im2col_step)
     out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+    if not value.is_cuda:  # C++ CPU backend, same C-ABI, NULL stream
+        _lib.call_cpu("gd_msda_forward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
+                      level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), N, S, M, D, L, Lq, P,
+                      out.data_ptr(), None)
+        return out
     nbytes = algorithmic_bytes("fwd", N, S, M, D, L, Lq, P, value.element_size())
     t0 = timer.begin() if timer is not None else None
     _lib.call("gd_msda_forward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
@@ -138,6 +157,11 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     grad_value = torch.empty((N, S, M, D), dtype=acc, device=value.device)
     grad_loc = torch.empty((N, Lq, M, L, P, 2), dtype=acc, device=value.device)
     grad_attn = torch.empty((N, Lq, M, L, P), dtype=acc, device=value.device)
+    if not value.is_cuda:  # C++ CPU backend, same C-ABI, NULL stream
+        _lib.call_cpu("gd_msda_backward", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
+                      level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), grad_output.data_ptr(),
+                      N, S, M, D, L, Lq, P, grad_value.data_ptr(), grad_loc.data_ptr(), grad_attn.data_ptr(), None)
+        return _finish_grads(value, sampling_loc, attn_weight, grad_value, grad_loc, grad_attn, grad_value_dtype)
     hs = None
     if host_shapes is not None and len(host_shapes) == L:
         hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
@@ -149,6 +173,10 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
               hs, _lib.stream_of(value), nbytes=nbytes)
     if t0 is not None:
         timer.end("bwd", Lq, nbytes, t0)
+    return _finish_grads(value, sampling_loc, attn_weight, grad_value, grad_loc, grad_attn, grad_value_dtype)
+
+
+def _finish_grads(value, sampling_loc, attn_weight, grad_value, grad_loc, grad_attn, grad_value_dtype):
     out_dtype = value.dtype if grad_value_dtype is None else grad_value_dtype
     if grad_value.dtype != out_dtype:
         grad_value = grad_value.to(out_dtype)

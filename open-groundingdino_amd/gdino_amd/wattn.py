@@ -26,14 +26,22 @@ copies (nor their backward) is launched.  A pad position's q/k/v is the qkv
 bias (the Linear of the zero pad row); its gradient is returned as the bias
 gradient, which autograd adds to the Linear's own.
 
-The HIP kernel covers N <= 64 (window <= 8) and hd = 32 (every Swin-T/S/B/L
-head) in fp32 and bf16.  Other shapes (Swin-B/384's 12x12 windows, N = 144)
-and dtypes use the torch composition (ROCm library kernels); CPU tensors
-raise, like every HIP op of this package.
+The HIP kernel covers N <= 144 (windows up to 12x12: Swin-T/S/B/L at 224 and
+Swin-B/L at 384) and hd = 32 (every Swin-T/S/B/L head) in fp32 and bf16.
+Other shapes and dtypes use the torch composition (ROCm library kernels);
+CPU tensors raise, like every HIP op of this package.
+
+When relative_position_index is the reference's (swin_transformer.py:104-115;
+checked once per buffer) the kernel is given NULL and computes the index
+itself, and a shift mask made by ``shifted_window_mask`` (the reference's
+region mask, :402-426) is passed as NULL to the image entry points, which then
+compute it from the geometry: neither the [N*N] int64 index nor the
+[nW, N, N] fp32 mask is read per window.
 """
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -45,7 +53,36 @@ _lib.register("gd_window_attn_backward", [_i, _p, _p, _p, _p, _p, _p, _p, _i, _i
 _lib.register("gd_window_attn_image_forward", [_i] + [_p] * 5 + [_i] * 7 + [_f, _p, _p, _p])
 _lib.register("gd_window_attn_image_backward", [_i] + [_p] * 8 + [_i] * 7 + [_f, _p, _p, _p, _p])
 
-MAX_TOKENS = 64
+MAX_TOKENS = 144
+
+_STD_INDEX = {}  # id(base tensor) -> (weakref to it, (version, numel, offset), is the reference index)
+
+
+def _kernel_index(rel_index: torch.Tensor, n: int):
+    """None (the kernel computes the index) when rel_index is the reference's
+    for a square window, else the int64 tensor; the comparison is made once
+    per buffer object and version (a host sync on first use only).  Keyed by
+    the base tensor (the module buffer behind the per-call .view(-1)), held
+    weakly, so a freed buffer's address reused by another tensor never hits."""
+    ws = int(round(n ** 0.5))
+    if ws * ws != n:
+        return rel_index.to(torch.int64).contiguous()
+    base = rel_index._base if rel_index._base is not None else rel_index
+    key = (base._version, rel_index.numel(), rel_index.storage_offset())
+    hit = _STD_INDEX.get(id(base))
+    if hit is None or hit[0]() is not base or hit[1] != key:
+        from models.GroundingDINO.backbone.swin_transformer import relative_position_index
+        std = bool(torch.equal(rel_index.detach().reshape(-1).cpu(), relative_position_index(ws, ws).reshape(-1)))
+        for k in [k for k, v in _STD_INDEX.items() if v[0]() is None]:
+            del _STD_INDEX[k]
+        hit = _STD_INDEX[id(base)] = (weakref.ref(base), key, std)
+    return None if hit[2] else rel_index.to(torch.int64).contiguous()
+
+
+def _is_region_mask(mask, hw, ws, shift) -> bool:
+    """mask is shifted_window_mask's region mask for this geometry"""
+    hp, wp = -(-hw[0] // ws) * ws, -(-hw[1] // ws) * ws
+    return getattr(mask, "_gd_region_mask", None) == (hp, wp, ws, shift)
 
 
 def supported(qkv: torch.Tensor) -> bool:
@@ -59,14 +96,14 @@ class WindowAttnFunction(torch.autograd.Function):
         _lib.require_device(qkv, table, rel_index, mask, what="window_attention")
         qkv = qkv.contiguous()
         table32 = table.detach().float().contiguous()
-        ridx = rel_index.to(torch.int64).contiguous()
-        mask32 = None if mask is None else mask.float().contiguous()
         b_, n, _, nh, hd = qkv.shape
+        ridx = _kernel_index(rel_index, n)
+        mask32 = None if mask is None else mask.float().contiguous()
         nw = 1 if mask32 is None else mask32.shape[0]
         out = torch.empty(b_, n, nh * hd, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(b_, nh, n, dtype=torch.float32, device=qkv.device)
         _lib.call("gd_window_attn_forward", _lib.dtype_code(qkv), qkv.data_ptr(), table32.data_ptr(),
-                  ridx.data_ptr(), _lib.ptr(mask32), b_, n, nh, hd, nw, float(scale), out.data_ptr(),
+                  _lib.ptr(ridx), _lib.ptr(mask32), b_, n, nh, hd, nw, float(scale), out.data_ptr(),
                   lse.data_ptr(), _lib.stream_of(qkv), flops=4.0 * b_ * nh * n * n * hd)
         ctx.save_for_backward(qkv, table32, ridx, mask32, out, lse)
         ctx.scale = float(scale)
@@ -82,7 +119,7 @@ class WindowAttnFunction(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         dtable = torch.zeros_like(table32)
         _lib.call("gd_window_attn_backward", _lib.dtype_code(qkv), qkv.data_ptr(), table32.data_ptr(),
-                  ridx.data_ptr(), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), b_, n, nh,
+                  _lib.ptr(ridx), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), b_, n, nh,
                   hd, nw, ctx.scale, dqkv.data_ptr(), dtable.data_ptr(), _lib.stream_of(qkv),
                   flops=10.0 * b_ * nh * n * n * hd)
         return dqkv, dtable.to(ctx.table_dtype), None, None, None
@@ -115,8 +152,10 @@ class WindowAttnImageFunction(torch.autograd.Function):
         qkv = qkv.contiguous()
         bias = None if qkv_bias is None else qkv_bias.detach().to(qkv.dtype).contiguous()
         table32 = table.detach().float().contiguous()
-        ridx = rel_index.to(torch.int64).contiguous()
-        mask32 = None if (mask is None or shift == 0) else mask.float().contiguous()
+        ridx = _kernel_index(rel_index, ws * ws)
+        # the region mask is computed by the kernel (NULL with shift > 0)
+        mask32 = (None if (mask is None or shift == 0 or _is_region_mask(mask, hw, ws, shift))
+                  else mask.float().contiguous())
         b, _, c3 = qkv.shape
         nh = table.shape[1]
         hd = c3 // (3 * nh)
@@ -124,7 +163,7 @@ class WindowAttnImageFunction(torch.autograd.Function):
         out = torch.empty(b, hw[0] * hw[1], c3 // 3, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(b * (hp // ws) * (wp // ws), nh, ws * ws, dtype=torch.float32, device=qkv.device)
         _lib.call("gd_window_attn_image_forward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
-                  table32.data_ptr(), ridx.data_ptr(), _lib.ptr(mask32), b, hw[0], hw[1], ws, shift, nh, hd,
+                  table32.data_ptr(), _lib.ptr(ridx), _lib.ptr(mask32), b, hw[0], hw[1], ws, shift, nh, hd,
                   float(scale), out.data_ptr(), lse.data_ptr(), _lib.stream_of(qkv),
                   flops=4.0 * lse.numel() * ws * ws * hd)  # windows x heads x N^2 x hd
         ctx.save_for_backward(qkv, bias, table32, ridx, mask32, out, lse)
@@ -143,7 +182,7 @@ class WindowAttnImageFunction(torch.autograd.Function):
         dbias = None if bias is None else torch.zeros(c3, dtype=torch.float32, device=qkv.device)
         dtable = torch.zeros_like(table32)
         _lib.call("gd_window_attn_image_backward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
-                  table32.data_ptr(), ridx.data_ptr(), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(),
+                  table32.data_ptr(), _lib.ptr(ridx), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(),
                   lse.data_ptr(), b, hw[0], hw[1], ws, shift, nh, c3 // (3 * nh), scale, dqkv.data_ptr(),
                   _lib.ptr(dbias), dtable.data_ptr(), _lib.stream_of(qkv),
                   flops=10.0 * lse.numel() * ws * ws * c3 // (3 * nh))

@@ -215,6 +215,9 @@ def shifted_window_mask(hp: int, wp: int, ws: int, shift: int, device) -> torch.
         win = window_partition(t, ws).reshape(-1, ws * ws)
         diff = win[:, None, :] - win[:, :, None]
         m = torch.where(diff != 0, torch.tensor(-100.0), torch.tensor(0.0)).to(device)
+        # the window attention kernel computes this mask from the geometry
+        # instead of reading it (gdino_amd/wattn.py)
+        m._gd_region_mask = (hp, wp, ws, shift)
         _MASK_CACHE[key] = m
     return m
 

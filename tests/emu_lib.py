@@ -136,7 +136,8 @@ def window_attn_forward(qkv, table, ridx, mask, scale):
     mask [nW, N, N] f32 or None -> out [B_, N, nH*hd], lse [B_, nH, N]."""
     B_, N, _, nH, hd = qkv.shape
     nW = 1 if mask is None else mask.shape[0]
-    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    qkv, table = qkv.contiguous(), table.float().contiguous()
+    ridx = None if ridx is None else ridx.to(torch.int64).contiguous()
     mask = None if mask is None else mask.float().contiguous()
     out = torch.empty(B_, N, nH * hd, dtype=qkv.dtype)
     lse = torch.empty(B_, nH, N, dtype=torch.float32)
@@ -149,7 +150,8 @@ def window_attn_backward(qkv, table, ridx, mask, scale, out, lse, grad_out):
     """-> grad_qkv (qkv dtype), grad_table (f32, [R, nH])."""
     B_, N, _, nH, hd = qkv.shape
     nW = 1 if mask is None else mask.shape[0]
-    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    qkv, table = qkv.contiguous(), table.float().contiguous()
+    ridx = None if ridx is None else ridx.to(torch.int64).contiguous()
     mask = None if mask is None else mask.float().contiguous()
     out, lse, grad_out = out.contiguous(), lse.contiguous(), grad_out.contiguous()
     gq = torch.full_like(qkv, float("nan"))
@@ -166,7 +168,8 @@ def window_attn_image_forward(qkv, qkv_bias, table, ridx, mask, hw, ws, shift, s
     b, _, c3 = qkv.shape
     nh = table.shape[1]
     hd = c3 // (3 * nh)
-    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    qkv, table = qkv.contiguous(), table.float().contiguous()
+    ridx = None if ridx is None else ridx.to(torch.int64).contiguous()
     bias = None if qkv_bias is None else qkv_bias.to(qkv.dtype).contiguous()
     mask = None if mask is None else mask.float().contiguous()
     hp, wp = -(-hw[0] // ws) * ws, -(-hw[1] // ws) * ws
@@ -184,7 +187,8 @@ def window_attn_image_backward(qkv, qkv_bias, table, ridx, mask, hw, ws, shift, 
     b, _, c3 = qkv.shape
     nh = table.shape[1]
     hd = c3 // (3 * nh)
-    qkv, table, ridx = qkv.contiguous(), table.float().contiguous(), ridx.to(torch.int64).contiguous()
+    qkv, table = qkv.contiguous(), table.float().contiguous()
+    ridx = None if ridx is None else ridx.to(torch.int64).contiguous()
     bias = None if qkv_bias is None else qkv_bias.to(qkv.dtype).contiguous()
     mask = None if mask is None else mask.float().contiguous()
     gq = torch.full_like(qkv, float("nan"))

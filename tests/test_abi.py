@@ -52,15 +52,22 @@ def test_python_binding_signatures_cover_header():
 
 
 def test_product_refuses_cpu_tensors():
+    """The HIP-only ops raise on host tensors (as the reference's CPU stub);
+    MSDA, which the reference dispatches by device, runs its C++ CPU backend
+    (tests/test_msda_cpu_backend.py)."""
     import torch
+    from gdino_amd.wattn import WindowAttnFunction
+    with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
+        WindowAttnFunction.apply(torch.zeros(2, 49, 3, 1, 32), torch.zeros(169, 1),
+                                 torch.zeros(49 * 49, dtype=torch.long), None, 1.0)
     from gdino_amd import msda
-    v = torch.zeros(1, 4, 1, 2)
+    v = torch.ones(1, 4, 1, 2)
     shapes = torch.tensor([[2, 2]])
     lsi = torch.tensor([0])
-    loc = torch.zeros(1, 1, 1, 1, 1, 2)
+    loc = torch.full((1, 1, 1, 1, 1, 2), 0.5)
     attn = torch.ones(1, 1, 1, 1, 1)
-    with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
-        msda.ms_deform_attn_forward(v, shapes, lsi, loc, attn, 64)
+    out = msda.ms_deform_attn_forward(v, shapes, lsi, loc, attn, 64)
+    assert torch.allclose(out, torch.ones(1, 1, 2))
 
 
 def test_msda_module_is_a_drop_in_for_the_reference_extension():

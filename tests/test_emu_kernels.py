@@ -238,9 +238,10 @@ t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 29, seed=13), 1e-5)
 t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=14, local=True, outlier_frac=0.1), 1e-5, host_shapes=t.MEDIUM)
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 2, 300, 40))
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 1, 130, 256))
-t.test_emulated_window_attention(7, 3, 8, 4, True, torch.float32, 1e-5)
-t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
-t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.float32, 1e-5)
+t.test_emulated_window_attention(7, 3, 8, 4, True, torch.float32, 1e-5, True)
+t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2, False)
+t.test_emulated_window_attention(12, 1, 3, 1, False, torch.bfloat16, 1.5e-2, True)
+t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.float32, 1e-5, True)
 t.test_emulated_attention(2, 2, 100, 130, 64, "bool", torch.float32, 1e-5, "lbh")
 print("sched-ok")
 """
@@ -289,11 +290,13 @@ t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
 t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
 t.test_emulated_msda_prologue(2, torch.bfloat16)
 t.test_emulated_msda_prologue(4, torch.float32)
-t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.bfloat16, 1.5e-2)
+t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.bfloat16, 1.5e-2, True)
+t.test_emulated_window_attention_image(1, 14, 17, 12, 6, 1, True, torch.bfloat16, 1.5e-2, False)
 """,
     r"""
-t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5)
-t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2)
+t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5, True)
+t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2, False)
+t.test_emulated_window_attention(12, 2, 4, 2, True, torch.float32, 1e-5, True)
 t.test_emulated_attention(2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh")
 t.test_emulated_attention(1, 1, 33, 300, 32, "add", torch.float32, 1e-5, "blh")
 t.test_emulated_attention_dropout(torch.float32, 1e-5)
@@ -355,16 +358,23 @@ def _wattn_ref(qkv, table, ridx, mask, scale):
     (3, 4, 6, 3, True, torch.float32, 1e-5),     # N = 9: mostly padding
     (7, 3, 8, 4, True, torch.bfloat16, 1.5e-2),  # the training dtype
     (5, 2, 20, 5, False, torch.bfloat16, 1.5e-2),
+    (12, 2, 4, 2, True, torch.float32, 1e-5),    # Swin-B/384: 12x12 windows, N = 144 (9 tiles)
+    (12, 1, 3, 1, False, torch.bfloat16, 1.5e-2),
+    (11, 1, 2, 1, False, torch.float32, 1e-5),   # N = 121: padded keys in the 9-tile kernel
 ])
-def test_emulated_window_attention(ws, nH, B_, nW, masked, dtype, tol):
+@pytest.mark.parametrize("std_index", [False, True], ids=["rel_index", "computed_index"])
+def test_emulated_window_attention(ws, nH, B_, nW, masked, dtype, tol, std_index):
+    """gd_window_attn_*: with the rel_index tensor, and with rel_index NULL
+    (the kernel computes the reference's index, swin_transformer.py:104-115)."""
     qkv, table, ridx, mask, scale, grad = _wattn_case(ws, nH, B_, nW, masked, seed=ws * 100 + B_, dtype=dtype)
-    out, lse = E.window_attn_forward(qkv, table, ridx, mask, scale)
+    kidx = None if std_index else ridx
+    out, lse = E.window_attn_forward(qkv, table, kidx, mask, scale)
     qd = qkv.double().requires_grad_(True)
     td = table.double().requires_grad_(True)
     ref = _wattn_ref(qd, td, ridx, None if mask is None else mask.double(), scale)
     assert E.rel_err(out.double(), ref.detach()) < tol
     ref.backward(grad.double())
-    gq, gt = E.window_attn_backward(qkv, table, ridx, mask, scale, out, lse, grad)
+    gq, gt = E.window_attn_backward(qkv, table, kidx, mask, scale, out, lse, grad)
     assert torch.isfinite(gq).all()
     assert E.rel_err(gq.double(), qd.grad) < tol * 2
     assert E.rel_err(gt.double(), td.grad) < tol * 2
@@ -374,9 +384,11 @@ def test_emulated_window_attention_rejects_bad_shapes():
     qkv, table, ridx, mask, scale, _ = _wattn_case(7, 2, 8, 4, True, 0, torch.float32)
     with pytest.raises(RuntimeError, match="multiple of nW"):
         E.window_attn_forward(qkv[:6], table, ridx, mask, scale)
-    big = torch.zeros(2, 81, 3, 1, 32)
+    big = torch.zeros(2, 169, 3, 1, 32)
     with pytest.raises(RuntimeError, match="bad sizes"):
-        E.window_attn_forward(big, torch.zeros(289, 1), torch.zeros(81 * 81, dtype=torch.long), None, 1.0)
+        E.window_attn_forward(big, torch.zeros(625, 1), torch.zeros(169 * 169, dtype=torch.long), None, 1.0)
+    with pytest.raises(RuntimeError, match="square window"):  # computed index needs N = ws^2
+        E.window_attn_forward(torch.zeros(2, 10, 3, 1, 32), torch.zeros(49, 1), None, None, 1.0)
 
 
 @pytest.mark.parametrize("b,h,w,ws,shift,nH,bias,dtype,tol", [
@@ -386,8 +398,11 @@ def test_emulated_window_attention_rejects_bad_shapes():
     (1, 5, 9, 4, 2, 1, False, torch.float32, 1e-5),    # pad reads zeros (qkv_bias=False)
     (1, 9, 11, 7, 3, 3, True, torch.bfloat16, 1.5e-2),
     (2, 3, 10, 7, 0, 2, True, torch.bfloat16, 1.5e-2),  # H < window: one window row, mostly pad
+    (1, 14, 17, 12, 6, 2, True, torch.float32, 1e-5),   # Swin-B/384 12x12 windows, shifted + padded
+    (1, 14, 17, 12, 6, 1, True, torch.bfloat16, 1.5e-2),
 ])
-def test_emulated_window_attention_image(b, h, w, ws, shift, nH, bias, dtype, tol):
+@pytest.mark.parametrize("computed", [False, True], ids=["given_mask_index", "computed_mask_index"])
+def test_emulated_window_attention_image(b, h, w, ws, shift, nH, bias, dtype, tol, computed):
     """gd_window_attn_image_*: the pad / roll / partition / reverse / crop of
     SwinTransformerBlock.forward fused into the kernel's row map, against
     oracle.blocks.window_attention_image_ref in fp64 (the shift mask of
@@ -404,7 +419,10 @@ def test_emulated_window_attention_image(b, h, w, ws, shift, nH, bias, dtype, to
     mask = shifted_window_mask(hp, wp, ws, shift, "cpu") if shift else None
     grad = torch.randn(b, h * w, C, generator=g).to(dtype)
     scale = 32 ** -0.5
-    out, lse = E.window_attn_image_forward(qkv, qb, table, ridx, mask, (h, w), ws, shift, scale)
+    # computed: rel_index and mask NULL -- the kernel derives the reference's
+    # index and region mask (:402-426) from the geometry
+    kidx, kmask = (None, None) if computed else (ridx, mask)
+    out, lse = E.window_attn_image_forward(qkv, qb, table, kidx, kmask, (h, w), ws, shift, scale)
     qd = qkv.double().requires_grad_(True)
     bd = qb.double().requires_grad_(True) if bias else None
     td = table.double().requires_grad_(True)
@@ -413,7 +431,8 @@ def test_emulated_window_attention_image(b, h, w, ws, shift, nH, bias, dtype, to
     assert torch.isfinite(out.double()).all()  # every real token row written
     assert E.rel_err(out.double(), ref.detach()) < tol
     ref.backward(grad.double())
-    gq, gb, gt = E.window_attn_image_backward(qkv, qb, table, ridx, mask, (h, w), ws, shift, scale, out, lse, grad)
+    gq, gb, gt = E.window_attn_image_backward(qkv, qb, table, kidx, kmask, (h, w), ws, shift, scale, out, lse,
+                                              grad)
     assert torch.isfinite(gq.double()).all()
     assert E.rel_err(gq.double(), qd.grad) < tol * 2
     assert E.rel_err(gt.double(), td.grad) < tol * 2
@@ -426,9 +445,9 @@ def test_emulated_window_attention_image_rejects_bad_geometry():
     table, ridx = torch.zeros(169, 3), torch.zeros(49 * 49, dtype=torch.long)
     with pytest.raises(RuntimeError, match="shift"):
         E.window_attn_image_forward(qkv, None, table, ridx, None, (9, 9), 7, 7, 1.0)
-    with pytest.raises(RuntimeError, match="window 9"):
-        E.window_attn_image_forward(qkv, None, torch.zeros(289, 3), torch.zeros(81 * 81, dtype=torch.long), None,
-                                    (9, 9), 9, 0, 1.0)
+    with pytest.raises(RuntimeError, match="window 13"):
+        E.window_attn_image_forward(torch.zeros(1, 169, 96 * 3), None, torch.zeros(625, 3),
+                                    torch.zeros(169 * 169, dtype=torch.long), None, (13, 13), 13, 0, 1.0)
 
 
 # ------------------------------- masked multi-head attention (flash, MFMA)

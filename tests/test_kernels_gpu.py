@@ -98,6 +98,9 @@ def _wattn_inputs(ws, nh, b_, nw, masked, dtype, seed=0):
     (7, 5, 22, 1, False),       # tail blocks
     (3, 2, 6, 3, True),         # N = 9 (mostly padded tokens)
     (8, 4, 16, 4, True),        # N = 64 (no padding)
+    (12, 4, 968, 484, True),    # Swin-B/384 stage 0 at 1024x1024 bs=2 (12x12 windows, 9 tiles)
+    (12, 16, 50, 25, False),    # Swin-B/384 stage 2
+    (11, 2, 6, 3, True),        # N = 121: padded keys in the 9-tile kernel
 ])
 def test_window_attention_fwd_bwd(dtype, tol, ws, nh, b_, nw, masked):
     from gdino_amd.wattn import WindowAttnFunction
@@ -119,16 +122,32 @@ def test_window_attention_fwd_bwd(dtype, tol, ws, nh, b_, nw, masked):
     assert _rel(tg.grad.cpu(), td.grad) < tol * 3
 
 
-def test_window_attention_op_dispatch_and_fallback():
-    """window_attention_packed runs the HIP kernel for N <= 64 and the torch
-    composition for Swin-B/384's 12x12 windows; both agree with the oracle."""
-    from gdino_amd import kernels
+def test_window_attention_op_dispatch_and_index_paths():
+    """window_attention_packed runs the HIP kernel for 7x7 and Swin-B/384's
+    12x12 windows (the reference index is computed by the kernel), a
+    non-standard rel_index tensor is read as given, and head_dim != 32 takes
+    the torch composition; all agree with the oracle."""
+    from gdino_amd import _lib, kernels
     from oracle.blocks import window_attention_packed_ref
     for ws in (7, 12):
         qkv, table, ridx, mask = _wattn_inputs(ws, 4, 8, 4, True, torch.float32, seed=ws)
-        out = kernels.window_attention_packed(qkv.to(DEV), table.to(DEV), ridx.to(DEV), mask.to(DEV), 32 ** -0.5)
-        ref = window_attention_packed_ref(qkv.double(), table.double(), ridx, mask.double(), 32 ** -0.5)
-        assert _rel(out.cpu(), ref) < 1e-3, ws
+        odd = (ridx * 7 + 3) % table.shape[0]  # not the reference index: the tensor path
+        for idx in (ridx, odd):
+            _lib.call_timer = ct = _lib.CallTimer()
+            try:
+                out = kernels.window_attention_packed(qkv.to(DEV), table.to(DEV), idx.to(DEV), mask.to(DEV),
+                                                      32 ** -0.5)
+            finally:
+                _lib.call_timer = None
+            ref = window_attention_packed_ref(qkv.double(), table.double(), idx, mask.double(), 32 ** -0.5)
+            assert _rel(out.cpu(), ref) < 1e-3, ws
+            assert "gd_window_attn_forward" in ct.summary(), ws
+    qkv = torch.randn(4, 49, 3, 2, 16, device=DEV)
+    table = torch.randn(169, 2, device=DEV)
+    ridx = _wattn_inputs(7, 2, 4, 1, False, torch.float32)[2]
+    out = kernels.window_attention_packed(qkv, table, ridx.to(DEV), None, 0.25)
+    ref = window_attention_packed_ref(qkv.double().cpu(), table.double().cpu(), ridx, None, 0.25)
+    assert _rel(out.cpu(), ref) < 1e-3
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1.5e-2)])
@@ -136,6 +155,8 @@ def test_window_attention_op_dispatch_and_fallback():
     (2, 25, 42, 7, 3, 3, True),   # Swin-T stage-0 geometry at 100x168 px: shifted, padded both ways
     (1, 14, 21, 7, 0, 6, True),   # exact tiling, W-MSA
     (1, 13, 9, 7, 3, 4, False),   # qkv_bias=False: pad rows read zeros
+    (2, 64, 64, 12, 6, 4, True),  # Swin-B/384 stage 0 at 256x256 px: 12x12 windows, shifted, padded
+    (1, 11, 25, 12, 0, 8, True),  # 12x12, H < window
 ])
 def test_window_attention_image_fwd_bwd(dtype, tol, b, h, w, ws, shift, nh, bias):
     """The Swin block's pad / roll / partition / reverse / crop fused into the
