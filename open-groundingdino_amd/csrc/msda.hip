@@ -132,21 +132,31 @@ extern "C" gd_status gd_msda_forward(gd_dtype dt, const void* value,
   hipStream_t s = as_hip(stream);
   const int64_t total = units * D;
 
-  const bool vec_ok = D == 32 && L == 4 && P == 4 && units < (int64_t(1) << 31) &&
+  // 32-bit byte offsets from the value base inside msda_fwd_vec
+  const size_t vbytes = size_t(N) * S * M * D * (dt == GD_BF16 ? 2 : 4);
+  const bool vec_ok = D == 32 && L == 4 && P == 4 && units < (int64_t(1) << 31) && vbytes < (size_t(1) << 32) &&
                       aligned16(value) && aligned16(loc) && aligned16(attn) && aligned16(out);
+  // gather batching: SB samples' corner loads issued together (GD_MSDA_FWD_SB
+  // 4, 8, or 40 / 80 = 4 / 8 with the next batch in flight while one is
+  // consumed).  Measured at 800x1333 bs=2 (tools/msda_microbench.py
+  // --fwd-variants): bf16 encoder 99 / 91 / 96 / 85 us
+  // (round 1: 128 us), fp32 120 / 120 / 127 / 138 us.
+  const int sb = env_int("GD_MSDA_FWD_SB", dt == GD_BF16 ? 80 : 4);
   if (dt == GD_F32 && vec_ok) {
     constexpr int UPW = 64 / (32 / 4);
     const int blocks = int((units + 4 * UPW - 1) / (4 * UPW));
-    hipLaunchKernelGGL((msda_fwd_vec<float, 32, 4, 4>), dim3(blocks), dim3(256), 0, s,
-                     (const float*)value, shapes, lsi, (const float*)loc, (const float*)attn,
-        (float*)out, S, Lq, M, int(units));
+#define GD_FWD_LAUNCH(T, SB)                                                                               \
+  hipLaunchKernelGGL((msda_fwd_vec<T, 32, 4, 4, (SB >= 10 ? SB / 10 : SB), (SB >= 10)>), dim3(blocks), dim3(256), 0, s, (const T*)value, shapes, \
+                     lsi, (const float*)loc, (const float*)attn, (T*)out, S, Lq, M, int(units))
+    if (sb == 8) GD_FWD_LAUNCH(float, 8); else if (sb == 40) GD_FWD_LAUNCH(float, 40);
+    else if (sb == 80) GD_FWD_LAUNCH(float, 80); else GD_FWD_LAUNCH(float, 4);
     GD_LAUNCH_CHECK("msda_fwd_vec<f32>");
   } else if (dt == GD_BF16 && vec_ok) {
     constexpr int UPW = 64 / (32 / 8);
     const int blocks = int((units + 4 * UPW - 1) / (4 * UPW));
-    hipLaunchKernelGGL((msda_fwd_vec<uint16_t, 32, 4, 4>), dim3(blocks), dim3(256), 0, s,
-                     (const uint16_t*)value, shapes, lsi, (const float*)loc, (const float*)attn,
-        (uint16_t*)out, S, Lq, M, int(units));
+    if (sb == 8) GD_FWD_LAUNCH(uint16_t, 8); else if (sb == 40) GD_FWD_LAUNCH(uint16_t, 40);
+    else if (sb == 80) GD_FWD_LAUNCH(uint16_t, 80); else GD_FWD_LAUNCH(uint16_t, 4);
+#undef GD_FWD_LAUNCH
     GD_LAUNCH_CHECK("msda_fwd_vec<bf16>");
   } else if (dt == GD_F32) {
     hipLaunchKernelGGL((msda_fwd_generic<float, float>), dim3(grid_for(total, 256)), dim3(256), 0, s,

@@ -148,6 +148,8 @@ HBM_PEAK = 8.0e12  # B/s, same table
 
 CPU_LIB_PATH = os.environ.get("GDINO_CPU_LIB", os.path.join(_HERE, "lib", "libgdino_cpu.so"))
 _cpu_lib = None
+# the MSDA core: the only entry points the CPU backend exports
+_CPU_ENTRY_POINTS = ("gd_msda_forward", "gd_msda_backward", "gd_msda_backward_geom")
 
 
 def cpu_lib() -> ctypes.CDLL:
@@ -162,11 +164,10 @@ def cpu_lib() -> ctypes.CDLL:
                 raise RuntimeError(f"gdino_amd: CPU backend not found at {CPU_LIB_PATH}; build it with "
                                    "make -C open-groundingdino_amd/csrc")
             handle = ctypes.CDLL(CPU_LIB_PATH, mode=ctypes.RTLD_LOCAL)
-            for name, argtypes in _SIGNATURES.items():
-                if name.startswith("gd_msda_"):
-                    fn = getattr(handle, name)
-                    fn.argtypes = argtypes
-                    fn.restype = ctypes.c_int
+            for name in _CPU_ENTRY_POINTS:
+                fn = getattr(handle, name)
+                fn.argtypes = _SIGNATURES[name]
+                fn.restype = ctypes.c_int
             handle.gd_last_error.restype = ctypes.c_char_p
             handle.gd_runtime_info.restype = ctypes.c_char_p
             if handle.gd_abi_version() != 1:

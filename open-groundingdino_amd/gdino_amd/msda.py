@@ -75,7 +75,7 @@ def _on_host(*tensors) -> bool:
     every one is on the ROCm device; raise on a mix."""
     devs = {t.is_cuda for t in tensors if t is not None}
     if len(devs) > 1:
-        raise RuntimeError("ms_deform_attn: tensors must all be on the same device (host or ROCm)")
+        raise RuntimeError("ms_deform_attn: tensors must all be on one device, the CPU (host backend) or the ROCm device")
     return devs == {False}
 
 

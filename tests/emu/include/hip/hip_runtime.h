@@ -331,6 +331,8 @@ void launch(dim3 g, dim3 b, F&& f) {
 #define __syncthreads() ::gd_emu::syncthreads()
 #define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
 #define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
+// compiler scheduling hints: no semantics to emulate
+#define __builtin_amdgcn_sched_barrier(mask) ((void)(mask))
 #define __builtin_amdgcn_ds_read_tr16_b64_v4i16(p) ::gd_emu::ds_read_tr16_b64((const void*)(uintptr_t)(p))
 #define __builtin_amdgcn_ds_swizzle(v, pattern) ::gd_emu::ds_swizzle((v), (pattern))
 #define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) \

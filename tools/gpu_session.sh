@@ -65,6 +65,23 @@ core)
   python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
       --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
   ;;
+final)
+  # MSDA forward batching variants, parity, the default and forward-only
+  # bench lines, trace + PMC passes
+  step "pytest -m gpu"
+  T 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > gpurun_out/s_gpu_tests.log 2>&1 &&
+  step "bench (default)" &&
+  T 600 python3 bench.py > gpurun_out/s_bench.log 2>&1 &&
+  step "bench (forward only, config 2)" &&
+  T 600 python3 bench.py --no-cpu-baseline --forward-only > gpurun_out/s_bench_fwd.log 2>&1 &&
+  prof_trace s_prof --steps 3 --warmup 2 &&
+  prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&
+  prof_pmc s_pmc_write WRITE_SIZE --steps 1 --warmup 1 &&
+  step "pmc_traffic" &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
+      --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
+  ;;
 prof)
   prof_trace s_prof --steps 3 --warmup 2 &&
   prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&

@@ -141,12 +141,42 @@ def enc_variants(iters, variants=None):
                                   frac=bb / t / PEAK, rel_err_vs_lane32=err)), flush=True)
 
 
+def fwd_variants(iters):
+    """Forward (bs=2, 800x1333) under each gather batching of msda_fwd_vec
+    (GD_MSDA_FWD_SB), encoder shape on the init geometry and a 2-px spread,
+    decoder shape on uniform random locations; outputs compared with the
+    first variant (bit-identical expected: same arithmetic order)."""
+    S = sum(h * w for h, w in LEVELS)
+    for vd in (torch.bfloat16, torch.float32):
+        for lq, geom in ((S, "init"), (S, "spread2"), (900, "uniform")):
+            v, sh, ls, loc, attn, go = inputs(lq, vd)
+            if geom == "init":
+                loc = init_geometry_loc(2)
+            ref = None
+            for sb in ("4", "8", "40", "80"):
+                os.environ["GD_MSDA_FWD_SB"] = sb
+                fn = lambda: msda.ms_deform_attn_forward(v, sh, ls, loc, attn, 64)  # noqa: E731
+                out = fn()
+                torch.cuda.synchronize()
+                ref = out.clone() if ref is None else ref
+                same = bool(torch.equal(out, ref))
+                t = time_it(fn, iters)
+                bf = algo_bytes(2, S, lq, v.element_size())
+                print(json.dumps(dict(dtype=str(vd).split(".")[-1], lq=lq, geom=geom, sb=sb, fwd_us=t * 1e6,
+                                      GBps=bf / t / 1e9, frac=bf / t / PEAK, identical=same)), flush=True)
+            os.environ.pop("GD_MSDA_FWD_SB", None)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--fwd-variants", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--enc-variants", action="store_true")
     ap.add_argument("--enc-probes", action="store_true")
     args = ap.parse_args()
+    if args.fwd_variants:
+        fwd_variants(args.iters)
+        return
     if args.enc_variants or args.enc_probes:
         enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[2]] + ENC_PROBES if args.enc_probes else None)
         return
