@@ -237,7 +237,9 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
                      (float*)grad_loc, (float*)grad_attn, S, M, tl, rmax, mode)
 #define GD_ENC_LAUNCH_ROWS(T)                  \
   if (rows <= 160) GD_ENC_LAUNCH(T, 160);      \
-  else if (rows <= 256) GD_ENC_LAUNCH(T, 256); \
+  else if (rows <= 224) GD_ENC_LAUNCH(T, 224); \
+  else if (rows <= 288) GD_ENC_LAUNCH(T, 288); \
+  else if (rows <= 352) GD_ENC_LAUNCH(T, 352); \
   else if (rows <= 512) GD_ENC_LAUNCH(T, 512); \
   else GD_ENC_LAUNCH(T, 1024)
       if (dt == GD_F32) {

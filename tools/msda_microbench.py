@@ -103,6 +103,19 @@ ENC_VARIANTS = [
     ("enc 2x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "2x8,2x8,2x4,2x4", "GD_MSDA_ENC_CAP": "60,40,28,28"}),
 ]
 ENC_PROBES = []
+# larger level boxes: fewer corners outside the box (direct 128-B atomics);
+# simulated atomic bytes at the init geometry 572 (default) / 448 / 403 / 393 MB
+ENC_CAPS = [
+    ("enc 4x4 cap96", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x4,4x4,4x4,4x4", "GD_MSDA_ENC_CAP": "96,48,32,32"}),
+    ("enc 4x4 cap128", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x4,4x4,4x4,4x4",
+                        "GD_MSDA_ENC_CAP": "128,64,40,40"}),
+    ("enc 4x4 cap160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x4,4x4,4x4,4x4",
+                        "GD_MSDA_ENC_CAP": "160,64,48,48"}),
+    ("enc 4x8 cap160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "4x8,4x8,4x8,4x8",
+                        "GD_MSDA_ENC_CAP": "160,64,40,40"}),
+    ("enc 8x8 cap320", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "8x8,8x8,8x8,8x8",
+                        "GD_MSDA_ENC_CAP": "320,128,48,48"}),
+]
 
 
 def enc_variants(iters, variants=None):
@@ -173,9 +186,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--enc-variants", action="store_true")
     ap.add_argument("--enc-probes", action="store_true")
+    ap.add_argument("--enc-caps", action="store_true")
     args = ap.parse_args()
     if args.fwd_variants:
         fwd_variants(args.iters)
+        return
+    if args.enc_caps:
+        enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[1]] + ENC_CAPS)
         return
     if args.enc_variants or args.enc_probes:
         enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[2]] + ENC_PROBES if args.enc_probes else None)
