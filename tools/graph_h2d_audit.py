@@ -7,11 +7,12 @@ moves a tensor across devices (_to_copy / copy_ with a device change).
 Inside a HIP-graph capture the first kind becomes a memcpy node whose host
 source (a temporary staging buffer) does not outlive the capture -- a replay
 then reads memory that is no longer mapped -- and the second kind is illegal.
-Runs on the CPU (the HIP-only ops routed to their oracles, as the CPU tests
-do), so it needs no GPU: device changes cannot show here, host-data
-creation and scalar reads can.
+On the CPU (default) the HIP-only ops are routed to their oracles, as the
+CPU tests do: device changes cannot show there, host-data creation and
+scalar reads can.  With --device cuda the HIP path itself runs under bf16
+autocast, as bench.py's train step does.
 
-    python tools/graph_h2d_audit.py [--height H --width W]
+    python tools/graph_h2d_audit.py [--device cuda] [--height H --width W]
 """
 import argparse
 import os
@@ -57,20 +58,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=320)
+    ap.add_argument("--device", default="cpu")
     a = ap.parse_args()
-    from oracle_hooks import oracle_msda
+    dev = torch.device(a.device)
+    if dev.type == "cpu":
+        from oracle_hooks import oracle_msda
+        route = oracle_msda
+    else:
+        def route():
+            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
 
     from gdino_amd.config import make_args
     from gdino_amd.train import build_training, synthetic_batch
 
     torch.manual_seed(0)
-    args = make_args(device="cpu")
-    model, criterion, _, _ = build_training(args, torch.device("cpu"))
+    args = make_args(device=str(dev))
+    model, criterion, _, _ = build_training(args, dev)
     model.train()
     samples, targets, captions, cats = synthetic_batch(2, a.height, a.width, n_boxes=4, n_tokens=64, seed=0,
-                                                       device="cpu")
-    with oracle_msda():
-        text, _ = model.prepare_text(captions, torch.device("cpu"))
+                                                       device=dev)
+    with route():
+        text, _ = model.prepare_text(captions, dev)
         inputs = (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"], text["text_token_mask"],
                   text["self_masks"], text["position_ids"])
         model.forward_core(*inputs)  # warm-up: device constants are built here, as in the capture's warm-up

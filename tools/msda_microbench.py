@@ -102,7 +102,15 @@ ENC_VARIANTS = [
                             "GD_MSDA_ENC_CAP": "76,32,24,24", "GD_MSDA_ENC_RMAX": "4"}),
     ("enc 2x8 r160", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_TILE": "2x8,2x8,2x4,2x4", "GD_MSDA_ENC_CAP": "60,40,28,28"}),
 ]
-ENC_PROBES = []
+# where the time goes: each probe drops one phase (wrong gradients; timing only)
+ENC_PROBES = [
+    ("enc no-direct", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "4"}),
+    ("enc no-flush", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "8"}),
+    ("enc no-lds-acc", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "16"}),
+    ("enc no-zero", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "32"}),
+    ("enc no-atomics", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "12"}),
+    ("enc gathers+reduce only", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "60"}),
+]
 # larger level boxes: fewer corners outside the box (direct 128-B atomics);
 # simulated atomic bytes at the init geometry 572 (default) / 448 / 403 / 393 MB
 ENC_CAPS = [
@@ -195,7 +203,7 @@ def main():
         enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[1]] + ENC_CAPS)
         return
     if args.enc_variants or args.enc_probes:
-        enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[2]] + ENC_PROBES if args.enc_probes else None)
+        enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[1]] + ENC_PROBES if args.enc_probes else None)
         return
     S = sum(h * w for h, w in LEVELS)
     res = []
