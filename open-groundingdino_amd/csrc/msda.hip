@@ -199,7 +199,7 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
              "msda_backward: null pointer");
   const int64_t total = units * D;
   const bool lane_ok = D == 32 && L == 4 && P == 4 && units < (int64_t(1) << 31) &&
-                       aligned16(loc) && aligned16(grad_loc);
+                       aligned16(loc) && aligned16(grad_loc) && aligned16(attn);
   // Self-attention (Lq == S: every value position is also a query, ordered as
   // the value rows, so consecutive queries sample neighbouring rows): tiled
   // backward with LDS pre-aggregation.  Cross-attention (the decoder's 900
