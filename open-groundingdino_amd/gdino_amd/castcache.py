@@ -82,15 +82,19 @@ def clear() -> None:
     _cache.clear()
 
 
-def _token_linear_ok(x, params, out_features, dt) -> bool:
-    """Route to gdino_amd.wgrad.token_linear (split-K weight gradient): the
-    GPU, bf16 autocast, trainable fp32 parameters, a qualifying shape."""
+def _token_linear_ok(x, params, out_features, dt):
+    """Route to gdino_amd.wgrad.token_linear: the GPU, bf16 autocast,
+    trainable fp32 parameters.  -> "splitk" (split-K weight-gradient kernel,
+    a qualifying token-heavy shape), "lib" (library GEMM with fp32 output) or
+    None (autocast's own path)."""
     if dt != torch.bfloat16 or not torch.is_grad_enabled() or _capturing(params[0]):
-        return False
+        return None
     if any(p.dtype != torch.float32 or not p.requires_grad for p in params):
-        return False
+        return None
     from . import wgrad
-    return wgrad.eligible(x, out_features, dt)
+    if wgrad.eligible(x, out_features, dt):
+        return "splitk"
+    return "lib" if wgrad.lib_eligible(x, dt) else None
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
@@ -100,9 +104,10 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
         wc = cached_cast(weight, dt)
         bc = None if bias is None else cached_cast(bias, dt)
         params = [weight] + ([bias] if bias is not None else [])
-        if _token_linear_ok(x, params, weight.shape[0], dt):
+        route = _token_linear_ok(x, params, weight.shape[0], dt)
+        if route is not None:
             from . import wgrad
-            return wgrad.token_linear(x, wc, bc, [weight], [] if bias is None else [bias])
+            return wgrad.token_linear(x, wc, bc, [weight], [] if bias is None else [bias], route == "lib")
         return F.linear(x, wc, bc)
     return F.linear(x, weight, bias)
 
@@ -157,9 +162,10 @@ def linear_shared_input(x: torch.Tensor, layers):
     b = _cached_cat([m.bias for m in layers], dt)
     from .misc import split_last
     params = [m.weight for m in layers] + [m.bias for m in layers]
-    if _token_linear_ok(x, params, w.shape[0], dt):
+    route = _token_linear_ok(x, params, w.shape[0], dt)
+    if route is not None:
         from . import wgrad
-        y = wgrad.token_linear(x, w, b, [m.weight for m in layers], [m.bias for m in layers])
+        y = wgrad.token_linear(x, w, b, [m.weight for m in layers], [m.bias for m in layers], route == "lib")
     else:
         y = F.linear(x, w, b)
     return list(split_last(y, [m.out_features for m in layers]))

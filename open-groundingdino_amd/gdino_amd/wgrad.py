@@ -17,6 +17,7 @@ when the shape qualifies (``eligible``); everything else is unchanged.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -32,6 +33,12 @@ _lib.register("gd_wgrad_batched", [_i, _p, _i64, _i64, _p, _i64, _i64, _i, _i, _
 
 MIN_TOKENS = 4096
 ENABLED = True
+# Linears below the split-K kernel's token threshold (decoder: 1 800 query
+# tokens, text: 512): dW through the library's bf16 x bf16 -> fp32 GEMM
+# (aten::mm.dtype) and db as an fp32-accumulated sum, straight into the fp32
+# parameters' gradients -- instead of autocast's bf16 dW / db plus a
+# bf16 -> fp32 cast kernel for each (GDINO_FP32_WGRAD=0: autocast's path)
+FP32_OUT_GEMM = os.environ.get("GDINO_FP32_WGRAD", "1") != "0"
 
 
 def eligible(x: torch.Tensor, out_features: int, dtype=None) -> bool:
@@ -73,6 +80,21 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, want_bias: bool):
     return dw, db
 
 
+def lib_eligible(x: torch.Tensor, dtype) -> bool:
+    """Route a (non split-K) Linear's weight gradient to weight_grad_lib."""
+    # a library GEMM (aten::mm.dtype exists for the ROCm device only): x.is_cuda,
+    # not _lib.on_device, which the host-side emulator tests redirect
+    return FP32_OUT_GEMM and dtype == torch.bfloat16 and x.is_cuda
+
+
+def weight_grad_lib(dy2: torch.Tensor, x2: torch.Tensor, want_bias: bool):
+    """dy2 [T, O], x2 [T, I] bf16 -> dW [O, I] fp32 (library GEMM with fp32
+    output), db [O] fp32 or None."""
+    dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+    db = dy2.sum(0, dtype=torch.float32) if want_bias else None
+    return dw, db
+
+
 def tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
     """a^T b over the token dimension (-2) with the split-K kernel?"""
     gran = 16 if a.dtype == torch.bfloat16 else 64
@@ -105,10 +127,11 @@ class TokenLinear(torch.autograd.Function):
     matching bias blocks); gradients go to ``params`` in fp32."""
 
     @staticmethod
-    def forward(ctx, x, wc, bc, nw, *params):
+    def forward(ctx, x, wc, bc, nw, lib_wgrad, *params):
         xc = x if x.dtype == wc.dtype else x.to(wc.dtype)
         y = F.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
+        ctx.lib_wgrad = lib_wgrad
         ctx.x_dtype = x.dtype
         ctx.rows = [p.shape[0] for p in params[:nw]]
         ctx.nw = nw
@@ -121,17 +144,18 @@ class TokenLinear(torch.autograd.Function):
         dy = dy.to(wc.dtype)
         dx = torch.matmul(dy, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
         i = xc.shape[-1]
-        dw, db = weight_grad(dy.reshape(-1, dy.shape[-1]).contiguous(), xc.reshape(-1, i).contiguous(),
-                             ctx.has_bias)
+        wg = weight_grad_lib if ctx.lib_wgrad else weight_grad
+        dw, db = wg(dy.reshape(-1, dy.shape[-1]).contiguous(), xc.reshape(-1, i).contiguous(), ctx.has_bias)
         grads = list(dw.split(ctx.rows, 0))
         if ctx.has_bias:
             grads += list(db.split(ctx.rows, 0))
-        return (dx, None, None, None, *grads)
+        return (dx, None, None, None, None, *grads)
 
 
-def token_linear(x, wc, bc, weights, biases):
+def token_linear(x, wc, bc, weights, biases, lib_wgrad=False):
     """F.linear(x, wc, bc) whose weight / bias gradients reach the fp32
     ``weights`` / ``biases`` (row blocks of wc / bc) through the split-K
-    kernel."""
+    kernel (or, lib_wgrad, the library GEMM with fp32 output)."""
     params = list(weights) + (list(biases) if bc is not None else [])
-    return TokenLinear.apply(x, wc.detach(), None if bc is None else bc.detach(), len(weights), *params)
+    return TokenLinear.apply(x, wc.detach(), None if bc is None else bc.detach(), len(weights), bool(lib_wgrad),
+                             *params)

@@ -405,6 +405,7 @@ def test_token_linear_matches_autocast_linear():
     res = {}
     for flag in (True, False):
         wgrad.ENABLED = flag
+        wgrad.FP32_OUT_GEMM = flag  # False: autocast's own Linear
         castcache.clear()
         lin.zero_grad()
         xi = x.clone().requires_grad_(True)
@@ -413,6 +414,7 @@ def test_token_linear_matches_autocast_linear():
         (y.float() * gy).sum().backward()
         res[flag] = (y.float(), lin.weight.grad.clone(), lin.bias.grad.clone(), xi.grad.clone())
     wgrad.ENABLED = True
+    wgrad.FP32_OUT_GEMM = True
     xd = x.detach().double().requires_grad_(True)
     wd = lin.weight.detach().double().requires_grad_(True)
     bd = lin.bias.detach().double().requires_grad_(True)
@@ -420,6 +422,43 @@ def test_token_linear_matches_autocast_linear():
     (yd * gy.double()).sum().backward()
     torch.testing.assert_close(res[True][0], res[False][0], rtol=0, atol=0)
     for k, ref in ((1, wd.grad), (2, bd.grad), (3, xd.grad)):
+        mine = _rel(res[True][k].cpu(), ref.cpu())
+        lib = _rel(res[False][k].cpu(), ref.cpu())
+        assert mine < 1e-2 and mine <= lib * 1.5 + 1e-6, (k, mine, lib)
+
+
+@pytest.mark.parametrize("t,i,o,bias", [(1800, 256, 2048, True), (1800, 2048, 256, True), (512, 256, 256, False),
+                                        (900, 256, 8, True)])
+def test_small_linear_fp32_weight_grad(t, i, o, bias):
+    """Below the split-K threshold (decoder / text Linears) castcache.linear
+    takes dW from the library's bf16 x bf16 -> fp32 GEMM and db from an fp32
+    sum (wgrad.weight_grad_lib): output bit-identical to autocast's Linear,
+    gradients within bf16 noise of it, both against fp64."""
+    from gdino_amd import castcache, wgrad
+    torch.manual_seed(t + o)
+    lin = torch.nn.Linear(i, o, bias=bias).to(DEV)
+    x = torch.randn(t, i, device=DEV)
+    gy = torch.randn(t, o, device=DEV)
+    res = {}
+    for flag in (True, False):
+        wgrad.FP32_OUT_GEMM = flag
+        castcache.clear()
+        lin.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = castcache.linear(xi, lin.weight, lin.bias)
+        (y.float() * gy).sum().backward()
+        res[flag] = [y.float(), lin.weight.grad.clone(), xi.grad.clone()] + ([lin.bias.grad.clone()] if bias else [])
+        assert lin.weight.grad.dtype == torch.float32
+    wgrad.FP32_OUT_GEMM = True
+    xd = x.detach().double().requires_grad_(True)
+    wd = lin.weight.detach().double().requires_grad_(True)
+    bd = lin.bias.detach().double().requires_grad_(True) if bias else None
+    yd = torch.nn.functional.linear(xd, wd, bd)
+    (yd * gy.double()).sum().backward()
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=0, atol=0)
+    refs = [wd.grad, xd.grad] + ([bd.grad] if bias else [])
+    for k, ref in enumerate(refs, start=1):
         mine = _rel(res[True][k].cpu(), ref.cpu())
         lib = _rel(res[False][k].cpu(), ref.cpu())
         assert mine < 1e-2 and mine <= lib * 1.5 + 1e-6, (k, mine, lib)
