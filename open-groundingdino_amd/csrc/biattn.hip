@@ -81,8 +81,15 @@ gd_status softmax_fwd(const void* s, const uint8_t* pad_v, const uint8_t* pad_l,
   float* col_inv = col_m + size_t(bh) * Tn;
   const int64_t nrows = int64_t(bh) * S;
   const int rblocks = int((nrows + 3) / 4);
-  hipLaunchKernelGGL((colstats_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
-                     (const T*)s, pad_v, H, S, Tn, pm, plp);
+  constexpr int VE = 16 / int(sizeof(T));
+  const int lpr = Tn / VE;
+  if (Tn % VE == 0 && lpr >= 2 && 256 % lpr == 0 && aligned_to(s, 16)) {
+    hipLaunchKernelGGL((colstats_vec_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
+                       (const T*)s, pad_v, H, S, Tn, pm, plp);
+  } else {
+    hipLaunchKernelGGL((colstats_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
+                       (const T*)s, pad_v, H, S, Tn, pm, plp);
+  }
   GD_LAUNCH_CHECK("biattn colstats");
   hipLaunchKernelGGL((colmerge_kernel), dim3((Tn + 63) / 64, bh), dim3(1024), 0, st,
                      pm, plp, nc, Tn, col_m, col_inv);
