@@ -111,8 +111,15 @@ gd_status softmax_bwd(const void* pv, const void* pl, const void* dpv, const voi
   float* csum = part + size_t(bh) * nc * Tn * 2;
   const int64_t nrows = int64_t(bh) * S;
   const int rblocks = int((nrows + 3) / 4);
-  hipLaunchKernelGGL((colsum_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
-                     (const T*)pl, (const T*)dpl, S, Tn, part);
+  constexpr int VE = 16 / int(sizeof(T));
+  const int lpr = Tn / VE;
+  if (Tn % VE == 0 && lpr >= 2 && 256 % lpr == 0 && aligned_to(pl, 16) && aligned_to(dpl, 16)) {
+    hipLaunchKernelGGL((colsum_vec_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
+                       (const T*)pl, (const T*)dpl, S, Tn, part);
+  } else {
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3(nc, bh), dim3(256), 0, st,
+                       (const T*)pl, (const T*)dpl, S, Tn, part);
+  }
   GD_LAUNCH_CHECK("biattn colsum");
   hipLaunchKernelGGL((colsum_merge_kernel), dim3((Tn + 63) / 64, bh), dim3(1024), 0, st,
                      part, nc, Tn, csum);

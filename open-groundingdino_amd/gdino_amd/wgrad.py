@@ -87,10 +87,23 @@ def lib_eligible(x: torch.Tensor, dtype) -> bool:
     return FP32_OUT_GEMM and dtype == torch.bfloat16 and x.is_cuda
 
 
+_MM_DTYPE_OK = True
+
+
 def weight_grad_lib(dy2: torch.Tensor, x2: torch.Tensor, want_bias: bool):
     """dy2 [T, O], x2 [T, I] bf16 -> dW [O, I] fp32 (library GEMM with fp32
-    output), db [O] fp32 or None."""
-    dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+    output), db [O] fp32 or None.  If this torch build's ROCm backend
+    rejects aten::mm.dtype, dW is the bf16 GEMM cast to fp32 -- autocast's
+    own numerics -- for the rest of the process."""
+    global _MM_DTYPE_OK
+    dw = None
+    if _MM_DTYPE_OK:
+        try:
+            dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+        except (RuntimeError, NotImplementedError, TypeError):
+            _MM_DTYPE_OK = False
+    if dw is None:
+        dw = torch.mm(dy2.t(), x2).float()
     db = dy2.sum(0, dtype=torch.float32) if want_bias else None
     return dw, db
 
