@@ -269,10 +269,13 @@ def test_encoder_tiled_matches_direct_atomic_kernel(monkeypatch):
     direct = _msda().ms_deform_attn_backward(*inputs, 64)
     for a, b in zip(tiled, direct):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
-    # grad_loc / grad_attn do not involve atomics: same arithmetic (up to the
-    # compiler's FMA contraction choices in the two kernels)
-    torch.testing.assert_close(tiled[1], direct[1], rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(tiled[2], direct[2], rtol=1e-6, atol=1e-7)
+    # grad_loc / grad_attn do not involve atomics: the same expressions, so
+    # they agree to fp32 rounding -- the compiler's FMA contraction differs
+    # between the kernels (the round-2 direct kernel selects zeroed corners
+    # instead of branching around them), which moves sums that nearly
+    # cancel by a few ulp of their terms (2.9e-6 at most on this input)
+    torch.testing.assert_close(tiled[1], direct[1], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(tiled[2], direct[2], rtol=1e-5, atol=1e-5)
 
 
 ENC_TILINGS = [None, "8x16,8x8,4x4,2x4", "4x16,3x8,2x4,1x4", "5x7,3x3,2x2,1x1"]
