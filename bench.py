@@ -239,6 +239,13 @@ def main(argv=None, device_type="cuda"):
         if world > 1 or a.forward_only:
             raise SystemExit("--graphs is single-GPU train-step only")
         print("warning: --graphs is experimental (DESIGN.md section 7)", file=sys.stderr, flush=True)
+        # GEMM library inside the captured region (GDINO_GRAPH_BLAS: "hipblaslt"
+        # or "cublas" = rocBLAS on ROCm)
+        blas = os.environ.get("GDINO_GRAPH_BLAS")
+        if blas:
+            torch.backends.cuda.preferred_blas_library(blas)
+            print(f"graphs: preferred BLAS library {torch.backends.cuda.preferred_blas_library()}",
+                  file=sys.stderr, flush=True)
         from gdino_amd import graphs
         text, _ = model.prepare_text(captions, device)
         graphs.capture(model, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],

@@ -231,10 +231,16 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
     if (ok && cover == S && blocks < (int64_t(1) << 31) && rows <= 1024) {
       const int rmax = env_int("GD_MSDA_ENC_RMAX", 8);
       const int mode = env_int("GD_MSDA_ENC_MODE", 0);  // 1: ds_add_f32 instead of read-modify-write
-#define GD_ENC_LAUNCH(T, NR)                                                                           \
-  hipLaunchKernelGGL((msda_bwd_enc<T, NR>), dim3(int(blocks)), dim3(128), 0, s, (const T*)value, shapes, \
-                     lsi, (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_value,   \
+      // gathers of 2 units in flight (default) or 1 (GD_MSDA_ENC_DEPTH=1)
+      const bool deep = env_int("GD_MSDA_ENC_DEPTH", 2) >= 2;
+#define GD_ENC_LAUNCH1(T, NR, DP)                                                                          \
+  hipLaunchKernelGGL((msda_bwd_enc<T, NR, DP>), dim3(int(blocks)), dim3(128), 0, s, (const T*)value, shapes, \
+                     lsi, (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_value,       \
                      (float*)grad_loc, (float*)grad_attn, S, M, tl, rmax, mode)
+#define GD_ENC_LAUNCH(T, NR)                                             \
+  do {                                                                   \
+    if (deep) GD_ENC_LAUNCH1(T, NR, true); else GD_ENC_LAUNCH1(T, NR, false); \
+  } while (0)
 #define GD_ENC_LAUNCH_ROWS(T)                  \
   if (rows <= 160) GD_ENC_LAUNCH(T, 160);      \
   else if (rows <= 224) GD_ENC_LAUNCH(T, 224); \
@@ -251,6 +257,7 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
       }
 #undef GD_ENC_LAUNCH_ROWS
 #undef GD_ENC_LAUNCH
+#undef GD_ENC_LAUNCH1
       return GD_OK;
     }
   }

@@ -104,6 +104,7 @@ ENC_VARIANTS = [
 ]
 # where the time goes: each probe drops one phase (wrong gradients; timing only)
 ENC_PROBES = [
+    ("enc depth1", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_DEPTH": "1"}),
     ("enc no-direct", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "4"}),
     ("enc no-flush", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "8"}),
     ("enc no-lds-acc", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "16"}),
@@ -139,7 +140,7 @@ def enc_variants(iters, variants=None):
         ref = None
         for name, env in variants:
             saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_ENC_RMAX", "GD_MSDA_ENC_CAP",
-                                                    "GD_MSDA_ENC_TILE", "GD_MSDA_ENC_MODE")}
+                                                    "GD_MSDA_ENC_TILE", "GD_MSDA_ENC_MODE", "GD_MSDA_ENC_DEPTH")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
