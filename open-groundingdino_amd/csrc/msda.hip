@@ -231,8 +231,10 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
     if (ok && cover == S && blocks < (int64_t(1) << 31) && rows <= 1024) {
       const int rmax = env_int("GD_MSDA_ENC_RMAX", 8);
       const int mode = env_int("GD_MSDA_ENC_MODE", 0);  // 1: ds_add_f32 instead of read-modify-write
-      // gathers of 2 units in flight (default) or 1 (GD_MSDA_ENC_DEPTH=1)
-      const bool deep = env_int("GD_MSDA_ENC_DEPTH", 2) >= 2;
+      // gathers of 1 unit in flight (default, measured 0.84 ms) or 2
+      // (GD_MSDA_ENC_DEPTH=2: 152 VGPR, 3 waves/SIMD; A/B in
+      // tools/msda_microbench.py --enc-probes)
+      const bool deep = env_int("GD_MSDA_ENC_DEPTH", 1) >= 2;
 #define GD_ENC_LAUNCH1(T, NR, DP)                                                                          \
   hipLaunchKernelGGL((msda_bwd_enc<T, NR, DP>), dim3(int(blocks)), dim3(128), 0, s, (const T*)value, shapes, \
                      lsi, (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_value,       \

@@ -104,7 +104,7 @@ ENC_VARIANTS = [
 ]
 # where the time goes: each probe drops one phase (wrong gradients; timing only)
 ENC_PROBES = [
-    ("enc depth1", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_DEPTH": "1"}),
+    ("enc depth2", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_DEPTH": "2"}),
     ("enc no-direct", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "4"}),
     ("enc no-flush", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "8"}),
     ("enc no-lds-acc", {"GD_MSDA_BWD": "enc", "GD_MSDA_ENC_MODE": "16"}),
