@@ -146,8 +146,12 @@ ENC_TILES = ["16x16,8x8,4x4,2x4", "4x16,3x8,2x4,1x4", "5x7,3x3,2x2,1x1"]
     (WIDE, 1, True, 0.02, 6.0),     # wide spread: boxes overflow the accumulator
 ])
 @pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
-def test_emulated_enc_backward_matches_oracle(levels, n, local, outliers, spread, vdtype, monkeypatch):
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_emulated_enc_backward_matches_oracle(levels, n, local, outliers, spread, vdtype, depth, monkeypatch):
+    """depth: units whose gathers are in flight (GD_MSDA_ENC_DEPTH; 1 is the
+    default, 2 the two-deep pipeline variant)."""
     monkeypatch.setenv("GD_MSDA_BWD", "enc")
+    monkeypatch.setenv("GD_MSDA_ENC_DEPTH", depth)
     S = sum(h * w for h, w in levels)
     inputs = _levels_inputs(levels, n, S, seed=S + 3 * n, vdtype=vdtype, local=local, spread_px=spread,
                             outlier_frac=outliers)
