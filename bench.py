@@ -1,7 +1,8 @@
 """bench.py — Grounding DINO (Swin-T + BERT-base) training throughput on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    (N > 1 under torchrun: one rank per process from RANK / LOCAL_RANK / WORLD_SIZE;
+     N > 1 without a torchrun environment: bench.py starts the N ranks itself)
 
 A step is one full training iteration of BASELINE config 3 (the metric's
 "train images/sec"): synthetic odvg batch of bs=2 images per GPU at 800x1333
@@ -42,8 +43,8 @@ LEVELS_800 = [(100, 167), (50, 84), (25, 42), (13, 21)]
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bs", type=int, default=2, help="images per GPU")
     ap.add_argument("--height", type=int, default=800)
     ap.add_argument("--width", type=int, default=1333)
@@ -56,6 +57,8 @@ def parse(argv=None):
                     help="replay forward_core (fwd+bwd) as HIP graphs (experimental, 1 GPU; DESIGN.md §7)")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
+    ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
+                    help=argparse.SUPPRESS)  # cpu: the CPU contract tests only (HIP ops routed by the test)
     return ap.parse_args(argv)
 
 
@@ -70,6 +73,29 @@ def use_tunableop(path):
     t.set_filename(path, False)
     if not t.read_file(path):
         raise RuntimeError(f"TunableOp could not read {path}")
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None):
+    """``--gpus N`` (N > 1) without a torchrun environment: start the N ranks
+    as children of ``torch.distributed.run`` on 127.0.0.1 and return their
+    exit code.  The parent never touches the GPU (it only imports torch), so
+    no HIP context exists here when the children start; rank 0's JSON line
+    reaches stdout directly.  ``script`` (default: this file) is what each
+    rank runs with ``argv``."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__),
+           *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
 
 
 def setup_dist(n, on_gpu=True):
@@ -174,6 +200,17 @@ def cpu_baseline(bs):
     }
 
 
+def _dist_stats(ms):
+    """p50 / p90 / min / max of per-step times (ms) plus the first and last
+    steps, so a drift over the timed steps is visible."""
+    if not ms:
+        return None
+    s = sorted(ms)
+    q = lambda f: s[min(len(s) - 1, int(f * len(s)))]  # noqa: E731
+    return {"p50": s[len(s) // 2], "p90": q(0.9), "min": s[0], "max": s[-1], "first": ms[0], "last": ms[-1],
+            "n": len(ms)}
+
+
 def pmc_traffic(kname, bs):
     """HBM bytes per launch of the dominant MSDA kernel from the newest
     profiles/*_pmc_traffic.json (tools/pmc_traffic.py over separate
@@ -197,11 +234,22 @@ def pmc_traffic(kname, bs):
     return pick(rows, key=lambda k: k["grid"])["traffic_bytes"]
 
 
-def main(argv=None, device_type="cuda"):
+def main(argv=None, device_type="cuda", child_script=None):
     """device_type="cpu" exists for tests/test_bench_contract.py only (the
     HIP ops are then routed to the oracle by the test); the bench itself
-    always runs on cuda."""
+    always runs on cuda.  ``--gpus N`` with no RANK in the environment
+    launches the N ranks itself (launch_ranks; ``child_script`` lets the CPU
+    test wrap each rank in its oracle routing)."""
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    device_type = a.device or device_type
+    if a.gpus > 1 and "RANK" not in os.environ:
+        if device_type != "cuda" and "--device" not in argv:
+            argv += ["--device", device_type]
+        rc = launch_ranks(a.gpus, argv, child_script)
+        if rc:
+            raise SystemExit(rc)
+        return
     on_gpu = device_type == "cuda"
     rank, world, local = setup_dist(a.gpus, on_gpu)
     device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
@@ -262,13 +310,28 @@ def main(argv=None, device_type="cuda"):
     sync()
     if world > 1:
         dist.barrier()
+    # per-step device-side boundaries: one event per step on the current
+    # stream (no host sync inside the timed loop); the host clock brackets the
+    # whole region as the contract asks
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if on_gpu else None
+    host_marks = []
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    if evs:
+        evs[0].record()
+    for i in range(a.steps):
         loss = step()
+        if evs:
+            evs[i + 1].record()
+        host_marks.append(time.perf_counter())
     sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if evs:
+        step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)]
+    else:
+        step_ms = [(b - a_) * 1e3 for a_, b in zip([t0] + host_marks[:-1], host_marks)]
+    step_stats = _dist_stats(step_ms)
     kern = msda.timer.summary()
     msda.timer = None
     if world > 1:
@@ -322,6 +385,9 @@ def main(argv=None, device_type="cuda"):
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
+            # per-step device time between consecutive step boundaries (HIP
+            # events on the launch stream; rank 0), p50 / p90 / max
+            "step_ms": step_stats,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -9,11 +9,19 @@ rows of MultiheadAttention.in_proj_weight) is never cached at all. In total
 that is several hundred cast launches per step on a launch-bound step.
 
 ``cached_cast(p, dtype)`` returns a bf16 copy of parameter ``p`` that stays
-valid while ``p._version`` is unchanged:
+valid while ``p._version`` is unchanged and, for a trainable parameter, no
+optimizer step has run since the copy was made:
 
-* The optimizer's in-place update bumps the version, so the copy is
-  refreshed once per step.
-* Frozen weights are cast once.
+* The fused AdamW kernel (``torch.optim.AdamW(fused=True)``, the bench's and
+  build_optimizer's optimizer) updates the parameters in place WITHOUT
+  bumping their version counters (the foreach path does bump them).  A
+  version check alone therefore served the step-1 weights forever: the
+  forward never saw an update (round-2 bug, found by comparing the eager
+  loss trajectory with the HIP-graph one, which bypasses this cache; pinned
+  by test_cast_cache_follows_fused_adamw_updates).  A global
+  optimizer-step post hook (every torch.optim.Optimizer) bumps a generation
+  counter, and copies of trainable parameters are valid for one generation.
+* Frozen weights (requires_grad False, e.g. the BERT) are cast once.
 
 The copy is produced by the same ``p.to(dtype)`` autocast would run, so the
 numerics are bit-identical. When grad mode is on the copy is created with its
@@ -32,6 +40,7 @@ import weakref
 import torch
 import torch.nn.functional as F
 from torch import nn
+from torch.optim.optimizer import register_optimizer_step_post_hook
 
 ENABLED = os.environ.get("GDINO_CAST_CACHE", "1") != "0"
 # one GEMM for Linears that read the same input (linear_shared_input)
@@ -40,6 +49,20 @@ FUSE_SHARED_INPUT = os.environ.get("GDINO_FUSE_PROJ", "1") != "0"
 # against the fp64 reference goldens
 FUSE_WITHOUT_AUTOCAST = False
 _cache: dict = {}
+_generation = 0
+
+
+def _on_optimizer_step(*_args, **_kwargs) -> None:
+    """Invalidate the copies of trainable parameters after any optimizer step."""
+    global _generation
+    _generation += 1
+
+
+register_optimizer_step_post_hook(_on_optimizer_step)
+
+
+def _gen(trainable: bool) -> int:
+    return _generation if trainable else -1
 
 
 def autocast_dtype(x: torch.Tensor):
@@ -67,11 +90,12 @@ def cached_cast(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     if _capturing(p):
         return p.to(dtype)
     key = id(p)
+    ver = (p._version, _gen(p.requires_grad))
     ent = _cache.get(key)
-    if ent is not None and ent[0]() is p and ent[1] == p._version and ent[2] == dtype and ent[3] == grad:
+    if ent is not None and ent[0]() is p and ent[1] == ver and ent[2] == dtype and ent[3] == grad:
         return ent[4]
     t = p.to(dtype)
-    _cache[key] = (weakref.ref(p), p._version, dtype, grad, t)
+    _cache[key] = (weakref.ref(p), ver, dtype, grad, t)
     if len(_cache) > 8192:  # drop entries of freed parameters
         for k in [k for k, v in _cache.items() if v[0]() is None]:
             del _cache[k]
@@ -138,7 +162,7 @@ def _cached_cat(params, dtype):
         return torch.cat(ps).to(dtype)
     grad = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
     key = ("cat",) + tuple(id(p) for p in ps)
-    vers = tuple(p._version for p in ps)
+    vers = tuple(p._version for p in ps) + (_gen(any(p.requires_grad for p in ps)),)
     ent = _cache.get(key)
     if ent is not None and all(r() is p for r, p in zip(ent[0], ps)) and ent[1] == vers and ent[2] == dtype \
             and ent[3] == grad:

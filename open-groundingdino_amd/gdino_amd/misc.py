@@ -24,6 +24,24 @@ def device_const(key, make, device) -> Tensor:
     return t
 
 
+def topk_indices(x: Tensor, k: int) -> Tensor:
+    """torch.topk(x, k, dim=1)[1] (two-stage proposal selection,
+    reference transformer.py:292-296), safe inside a captured HIP graph.
+
+    For slices of >= 20 000 elements PyTorch's topk switches to its
+    multi-block radix select, whose captured replay does not follow new
+    input data (tools/graph_topk_probe.py, profiles/r03_graph_topk_probe.log:
+    the replay on new scores returns a different index set than eager).
+    S = 22 223 encoder tokens at 800x1333 is above that switch, 6 800 at
+    512x640 is below it: the size dependence of the round-2 graph fault.
+    Under capture the selection is a stable descending sort and a slice:
+    the same indices in the same order for distinct values (ties: lowest
+    index first; topk leaves tie order unspecified)."""
+    if x.is_cuda and torch.cuda.is_current_stream_capturing():
+        return torch.sort(x, dim=1, descending=True, stable=True)[1][:, :k]
+    return torch.topk(x, k, dim=1)[1]
+
+
 class NestedTensor:
     """Batched images + padding mask (True on padded pixels).
     Contract of groundingdino/util/misc.py:399-480; the model also accepts any

@@ -153,8 +153,10 @@ class WindowAttnImageFunction(torch.autograd.Function):
         bias = None if qkv_bias is None else qkv_bias.detach().to(qkv.dtype).contiguous()
         table32 = table.detach().float().contiguous()
         ridx = _kernel_index(rel_index, ws * ws)
-        # the region mask is computed by the kernel (NULL with shift > 0)
-        mask32 = (None if (mask is None or shift == 0 or _is_region_mask(mask, hw, ws, shift))
+        # the region mask is computed by the kernel (NULL with shift > 0) --
+        # only in its computed-index variant: with a given rel_index tensor the
+        # kernel runs its generic mode, which reads the mask tensor
+        mask32 = (None if (mask is None or shift == 0 or (ridx is None and _is_region_mask(mask, hw, ws, shift)))
                   else mask.float().contiguous())
         b, _, c3 = qkv.shape
         nh = table.shape[1]

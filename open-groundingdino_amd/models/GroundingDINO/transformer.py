@@ -24,7 +24,7 @@ from torch import Tensor, nn
 from gdino_amd import kernels
 from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
-from gdino_amd.misc import device_const, inverse_sigmoid
+from gdino_amd.misc import device_const, inverse_sigmoid, topk_indices
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
@@ -164,7 +164,7 @@ class Transformer(nn.Module):
             topk_logits = kernels.contrastive_rowmax(output_memory, text_dict["encoded_text"],
                                                      text_dict["text_token_mask"])
             enc_coord = self.enc_out_bbox_embed(output_memory) + output_proposals
-            topk_proposals = torch.topk(topk_logits, self.num_queries, dim=1)[1]  # [bs, nq]
+            topk_proposals = topk_indices(topk_logits, self.num_queries)  # [bs, nq]
             idx4 = topk_proposals.unsqueeze(-1).expand(-1, -1, 4)
             refpoint_embed_undetach = torch.gather(enc_coord, 1, idx4)
             refpoint_embed_ = refpoint_embed_undetach.detach()

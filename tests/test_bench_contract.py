@@ -92,6 +92,28 @@ def test_bench_two_ranks_contract():
     assert "cpu_baseline" not in r0  # rank 0 at N=1 only
 
 
+def test_bench_self_launches_ranks_from_a_bare_environment(capfd, monkeypatch):
+    """``python bench.py --gpus 2`` as the driver may call it, with no torchrun
+    environment: bench.main starts the 2 ranks itself (torch.distributed.run on
+    127.0.0.1) and rank 0 prints the one line.  Here the ranks run on
+    CPU/gloo with the HIP-only ops routed to the oracle (tests/bench_cpu_rank.py)."""
+    import os
+    import bench
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_cpu_rank.py")
+    bench.main(["--gpus", "2", "--steps", "1", "--warmup", "1", "--height", "256", "--width", "320"],
+               device_type="cpu", child_script=child)
+    out = capfd.readouterr().out
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    r0 = json.loads(lines[0])
+    assert r0["n_gpus"] == 2 and r0["config"]["parallelism"] == "dp2" and r0["config"]["global_batch"] == 4
+    assert abs(r0["value"] - 4 / (r0["ms_per_step"] / 1e3)) < 1e-6 * r0["value"]
+    assert r0["step_ms"]["n"] == 1 and r0["step_ms"]["max"] > 0
+    assert "cpu_baseline" not in r0
+
+
 def test_pmc_traffic_matches_the_encoder_and_decoder_launch_by_grid(tmp_path, monkeypatch):
     """roofline.traffic: the committed PMC summary is matched by kernel name,
     the encoder call to its kernel's largest grid, the decoder call to the

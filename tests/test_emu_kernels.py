@@ -86,6 +86,27 @@ def test_emulated_verified_kernels_match_oracle(vdtype, tol):
     _check_bwd((value, shapes, lsi, loc, attn, grad_out), tol)
 
 
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+def test_emulated_forward_nonfinite_locations_add_zero(vdtype):
+    """NaN / +-Inf sampling locations are skipped samples (the reference's
+    bounds test is false for them), so the vectorised forward's output stays
+    finite and equals the oracle's (NaN fractions times a zero
+    corner gave NaN)."""
+    value, shapes, lsi, loc, attn, _ = _levels_inputs(MEDIUM, 2, 50, seed=3, vdtype=vdtype)
+    g = torch.Generator().manual_seed(3)
+    bad = torch.rand(loc.shape[:-1], generator=g) < 0.25
+    kinds = torch.randint(0, 3, loc.shape[:-1], generator=g)
+    fill = torch.where(kinds == 0, float("nan"), torch.where(kinds == 1, float("inf"), float("-inf")))
+    axis = torch.randint(0, 2, loc.shape[:-1], generator=g)
+    loc = loc.clone()
+    for a in (0, 1):
+        loc[..., a] = torch.where(bad & (axis == a), fill.to(loc.dtype), loc[..., a])
+    out = E.msda_forward(value, shapes, lsi, loc, attn)
+    ref = oracle.msda_forward(value.double().numpy(), shapes, lsi, loc.double(), attn.double())
+    assert np.isfinite(ref).all() and torch.isfinite(out).all()
+    assert E.rel_err(out.double(), ref) < (1e-5 if vdtype == torch.float32 else 1e-2)
+
+
 # ------------------------------------------- tiled (LDS) encoder backward
 @pytest.mark.parametrize("levels,n,local,outliers", [
     (SMALL, 1, False, 0.0),     # every level box fits: all-LDS path

@@ -196,6 +196,35 @@ def test_window_attention_image_fwd_bwd(dtype, tol, b, h, w, ws, shift, nh, bias
         assert _rel(bg.grad.cpu(), bd.grad) < tol * 3
 
 
+@pytest.mark.parametrize("standard", [True, False])
+def test_window_attention_image_region_mask_with_given_index(standard):
+    """Shifted block with the module's own region mask (the cached
+    shifted_window_mask tensor the kernel recognises and recomputes) and a
+    rel_index that is (True) or is not (False) the reference's: with a
+    non-standard index the kernel runs its generic mode, so the mask tensor
+    must be passed, not dropped (tokens must not attend across roll regions).
+    fp32, against the fp64 step-by-step oracle."""
+    from gdino_amd.wattn import WindowAttnImageFunction
+    from models.GroundingDINO.backbone.swin_transformer import relative_position_index, shifted_window_mask
+    from oracle.blocks import window_attention_image_ref
+    g = torch.Generator().manual_seed(7)
+    b, h, w, ws, shift, nh = 1, 19, 30, 7, 3, 2
+    c = 32 * nh
+    qkv = torch.randn(b, h * w, 3 * c, generator=g)
+    table = torch.randn((2 * ws - 1) ** 2, nh, generator=g) * 0.5
+    ridx = relative_position_index(ws, ws).reshape(-1)
+    if not standard:
+        ridx = ridx.flip(0).contiguous()
+    hp, wp = -(-h // ws) * ws, -(-w // ws) * ws
+    mask = shifted_window_mask(hp, wp, ws, shift, DEV)  # the cached, recognisable region mask
+    ref = window_attention_image_ref(qkv.double(), None, table.double(), ridx, mask.double().cpu(), (h, w), ws,
+                                     shift, 32 ** -0.5)
+    out = WindowAttnImageFunction.apply(qkv.to(DEV), None, table.to(DEV), ridx.to(DEV), mask, (h, w), ws, shift,
+                                        32 ** -0.5)
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < 1e-3
+
+
 def test_swin_block_fused_matches_windowed_path():
     """SwinTransformerBlock.forward with the fused op vs the step-by-step
     windowed path (_windowed_attention, the reference's sequence) on the GPU,

@@ -263,3 +263,46 @@ def test_weighted_loss_matches_the_per_term_sum():
         for k, gk in zip(wd, grads):
             want = torch.tensor(wd[k], dtype=ld[k].dtype)
             assert torch.equal(gk, want), k
+
+
+def test_cast_cache_follows_fused_adamw_updates(built):
+    """Fused AdamW updates parameters in place without bumping their version
+    counters; the cast cache must still serve the updated weights on the next
+    step.  Two train steps with the cache on and off (fp32-exact casts: same
+    bits) must give bit-identical second-step losses."""
+    import copy
+
+    from gdino_amd import castcache
+    from gdino_amd.train import synthetic_batch, train_step
+    args, model0, criterion, *_ = built
+    samples, targets, caps, cats = synthetic_batch(1, 128, 160, n_boxes=3, n_tokens=24, seed=2, device="cpu")
+    p = torch.nn.Parameter(torch.ones(3))
+    opt = torch.optim.AdamW([p], lr=0.1, fused=True)
+    p.grad = torch.ones(3)
+    v = p._version
+    opt.step()
+    assert p._version == v, "fused AdamW bumps versions now: the generation guard is still needed for foreach=False"
+    losses = {}
+    for enabled in (True, False):
+        castcache.ENABLED = enabled
+        castcache.FUSE_SHARED_INPUT = False  # same GEMMs both ways (bit-identical gradients)
+        castcache.clear()
+        model = copy.deepcopy(model0)
+        model.train()
+        for m in model.modules():  # deterministic: no dropout / drop-path
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+            if hasattr(m, "drop_prob"):
+                m.drop_prob = 0.0
+        opt = torch.optim.AdamW([q for q in model.parameters() if q.requires_grad], lr=1e-2, fused=True)
+        try:
+            with oracle_msda():
+                losses[enabled] = [float(train_step(model, criterion, opt, samples, targets, caps, cats))
+                                   for _ in range(2)]
+        finally:
+            castcache.ENABLED = True
+            castcache.FUSE_SHARED_INPUT = True
+            castcache.clear()
+    assert losses[True][0] == losses[False][0]
+    assert losses[True][1] == losses[False][1], losses
+    assert losses[True][1] != losses[True][0]

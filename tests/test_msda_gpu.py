@@ -390,3 +390,33 @@ def test_module_runs_and_backprops():
     out.float().sum().backward()
     assert out.shape == src.shape and torch.isfinite(src.grad).all()
     assert m.sampling_offsets.weight.grad is not None and m.value_proj.weight.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_forward_nonfinite_locations_add_zero(dtype):
+    """A NaN or +-Inf sampling location is skipped (adds 0) as in the
+    reference kernel's bounds test (.cuh:238-299, NaN compares false); the
+    vectorised forward's branchless gathers must not turn it into NaN * 0.
+    Against the C oracle on the same inputs (fp64)."""
+    g = torch.Generator().manual_seed(5)
+    shapes = torch.as_tensor([(16, 20), (8, 10), (4, 5), (2, 3)], dtype=torch.long)
+    lsi = torch.cat((shapes.new_zeros((1,)), shapes.prod(1).cumsum(0)[:-1]))
+    S = int(shapes.prod(1).sum())
+    value = torch.rand(2, S, 8, 32, generator=g).to(dtype).double()
+    loc = torch.rand(2, 37, 8, 4, 4, 2, generator=g, dtype=torch.float64)
+    bad = torch.rand(loc.shape[:-1], generator=g) < 0.2
+    kinds = torch.randint(0, 3, loc.shape[:-1], generator=g)
+    fill = torch.where(kinds == 0, float("nan"), torch.where(kinds == 1, float("inf"), float("-inf"))).double()
+    axis = torch.randint(0, 2, loc.shape[:-1], generator=g)
+    for a in (0, 1):
+        loc[..., a] = torch.where(bad & (axis == a), fill, loc[..., a])
+    attn = torch.rand(2, 37, 8, 4, 4, generator=g, dtype=torch.float64) + 1e-5
+    attn /= attn.sum((-1, -2), keepdim=True)
+    ref = oracle.msda_forward(value, shapes, lsi, loc, attn)
+    assert np.isfinite(ref).all()
+    out = _msda().ms_deform_attn_forward(value.to(DEV, dtype), shapes.to(DEV), lsi.to(DEV), loc.to(DEV, torch.float32),
+                                         attn.to(DEV, torch.float32), 64)
+    torch.cuda.synchronize()
+    o = out.double().cpu().numpy()
+    assert np.isfinite(o).all(), "non-finite location leaked NaN into the output"
+    assert _rel_err(o, ref) < (1e-3 if dtype == torch.float32 else 1e-2)

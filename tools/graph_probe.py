@@ -59,8 +59,27 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "both"
     if what == "check1":  # one mode per process
         mode = sys.argv[2]
-        loss, g = run(mode, make_args(device="cuda", fusion_droppath=0.0), check=True, h=512, w=640)
+        hw = [int(v) for v in sys.argv[3:5]] if len(sys.argv) > 4 else [512, 640]
+        loss, g = run(mode, make_args(device="cuda", fusion_droppath=0.0), check=True, h=hw[0], w=hw[1])
         torch.save({"loss": loss, "g": {k: v.cpu() for k, v in g.items()}}, f"/tmp/gp_{mode}.pt")
+        sys.exit(0)
+    if what == "traj1":  # per-step loss trajectory of one mode (same seeds as the other)
+        mode = sys.argv[2]
+        torch.manual_seed(0)
+        dev = torch.device("cuda")
+        model, crit, _, opt = build_training(make_args(device="cuda"), dev)
+        model.train()
+        samples, targets, caps, cats = synthetic_batch(2, 800, 1333, n_boxes=8, n_tokens=256, seed=1000, device=dev)
+        if mode == "graph":
+            text, _ = model.prepare_text(caps, dev)
+            graphs.capture(model, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
+                                   text["text_token_mask"], text["self_masks"], text["position_ids"]))
+        losses = [float(train_step(model, crit, opt, samples, targets, caps, cats)) for _ in range(12)]
+        print(f"[{mode}] losses " + " ".join(f"{v:.1f}" for v in losses), flush=True)
+        sys.exit(0)
+    if what == "traj":
+        for mode in ("eager", "graph"):
+            subprocess.run([sys.executable, __file__, "traj1", mode], check=True, timeout=400)
         sys.exit(0)
     if what == "time1":
         kw = {}
@@ -94,8 +113,9 @@ if __name__ == "__main__":
                 sys.exit(1)
         sys.exit(0)
     if what in ("check", "both"):
+        hw = sys.argv[2:4] if len(sys.argv) > 3 else ["512", "640"]
         for mode in ("eager", "graph"):
-            subprocess.run([sys.executable, __file__, "check1", mode], check=True, timeout=400)
+            subprocess.run([sys.executable, __file__, "check1", mode] + hw, check=True, timeout=400)
         e, g = torch.load("/tmp/gp_eager.pt"), torch.load("/tmp/gp_graph.pt")
         worst = max(((e["g"][n] - g["g"][n]).abs().max() / (e["g"][n].abs().max() + 1e-12)).item() for n in e["g"])
         print(f"check: loss eager {e['loss']:.4f} graph {g['loss']:.4f}; max rel grad diff {worst:.3e}", flush=True)
