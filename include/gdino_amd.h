@@ -156,6 +156,38 @@ gd_status gd_msda_backward_geom(gd_dtype value_dtype, const void* value,
                                 void* grad_attn_weight, const int64_t* spatial_shapes_host,
                                 gd_stream_t stream);
 
+/* The same backward without float atomics ("sorted": a per-sample pass for
+ * grad_sampling_loc / grad_attn_weight, then grad_value as a sum per
+ * destination row over an inverted index of the samples; csrc/msda_sorted.inc).
+ * Replaces the same reference entry (ms_deform_attn_cuda.cu:83-153,
+ * ms_deform_attn.h:46-61).  Requirements (else GD_ERR_UNSUPPORTED):
+ * value F32 or BF16, channels 32, num_levels 4, num_point 4, the HOST level
+ * shapes, level_start_index their cumulative sums (as the model builds it)
+ * and spatial_size == sum H*W.
+ *   grad_value_dtype  F32, or BF16 when value is BF16 (written directly:
+ *                     every row is written exactly once, no zero fill)
+ *   workspace         device memory of gd_msda_backward_workspace_bytes()
+ *   flags             GD_MSDA_DETERMINISTIC: every output bitwise
+ *                     reproducible (each grad_value row summed in sample
+ *                     order); 0: same sums, order of arrival inside a cell.
+ * gd_msda_backward_workspace_bytes returns 0 when the sorted backward does
+ * not apply to these sizes. */
+#define GD_MSDA_DETERMINISTIC 1
+size_t gd_msda_backward_workspace_bytes(gd_dtype value_dtype, int batch, int spatial_size, int num_heads,
+                                        int channels, int num_levels, int num_query, int num_point,
+                                        const int64_t* spatial_shapes_host, int flags);
+gd_status gd_msda_backward_sorted(gd_dtype value_dtype, const void* value,
+                                  const int64_t* spatial_shapes,
+                                  const int64_t* level_start_index,
+                                  const void* sampling_loc, const void* attn_weight,
+                                  const void* grad_output, int batch,
+                                  int spatial_size, int num_heads, int channels,
+                                  int num_levels, int num_query, int num_point,
+                                  void* grad_value, gd_dtype grad_value_dtype,
+                                  void* grad_sampling_loc, void* grad_attn_weight,
+                                  const int64_t* spatial_shapes_host, void* workspace,
+                                  size_t workspace_bytes, int flags, gd_stream_t stream);
+
 /*
  * MSDA prologue (ms_deform_attn.py:274-363): offsets [N, Lq, M*L*P*2] and
  * attention logits [N, Lq, M*L*P] (F32 or BF16, contiguous rows with the

@@ -43,6 +43,7 @@ namespace gd {
 namespace {
 #include "msda_kernels.inc"
 #include "msda_enc.inc"
+#include "msda_sorted.inc"
 
 constexpr int kTileQ = 32;      // queries per workgroup (one head)
 constexpr int kTileRows = 384;  // LDS accumulator rows (48 KB): 3 workgroups per CU
@@ -349,4 +350,160 @@ extern "C" gd_status gd_msda_backward(gd_dtype dt, const void* value,
                                       gd_stream_t stream) {
   return gd_msda_backward_geom(dt, value, shapes, lsi, loc, attn, grad_out, N, S, M, D, L, Lq, P,
                                grad_value, grad_loc, grad_attn, nullptr, stream);
+}
+
+// ---------------------------------------------------------------------------
+// Sorted backward (msda_sorted.inc): plan, workspace, launches
+// ---------------------------------------------------------------------------
+namespace gd {
+namespace {
+
+struct SortedPlan {
+  SortGeo G;
+  int ncells = 0, nsamples = 0, nb = 0, k1_blocks = 0;
+  size_t o_cnt = 0, o_off = 0, o_bsum = 0, o_ids = 0, o_scr = 0, bytes = 0;
+};
+
+inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// false: the sorted backward does not apply (the caller uses another kernel)
+bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, const int64_t* hs, int flags,
+                 SortedPlan& pl) {
+  if (!((dt == GD_F32 || dt == GD_BF16) && D == 32 && L == 4 && P == 4 && hs && N > 0 && M > 0 && Lq >= 0))
+    return false;
+  SortGeo& G = pl.G;
+  int64_t cover = 0, cpn = 0;
+  for (int l = 0; l < 4; ++l) {
+    const int64_t h = hs[2 * l], w = hs[2 * l + 1];
+    if (h <= 0 || w <= 0 || h > (1 << 20) || w > (1 << 20)) return false;
+    G.H[l] = int(h);
+    G.W[l] = int(w);
+    G.lsi[l] = int(cover);
+    G.cofs[l] = int(cpn);
+    cover += h * w;
+    cpn += (h + 1) * (w + 1);
+  }
+  if (cover != S) return false;
+  const int64_t units = int64_t(N) * Lq * M;
+  const int64_t ncells = int64_t(N) * M * cpn;
+  const size_t vbytes = size_t(N) * S * M * D * (dt == GD_BF16 ? 2 : 4);
+  if (units * 16 >= (int64_t(1) << 31) || ncells + 1 >= (int64_t(1) << 31) || vbytes >= (size_t(1) << 32))
+    return false;
+  G.cpn = int(cpn);
+  G.N = N;
+  // K4 splits: about 24-48 entries per lane group (a pixel is a corner of
+  // 4 cells; a level-l cell holds ~Lq * P / (H W) samples of each (n, m))
+  const int lpu = dt == GD_BF16 ? 4 : 8, gpb = 256 / lpu, maxF = 64 / lpu;
+  int64_t bl = 0;
+  for (int l = 0; l < 4; ++l) {
+    const double e = 4.0 * double(Lq) * P / (double(G.H[l]) * G.W[l]);
+    int F = 1;
+    while (F < maxF && e / F > 48.0) F *= 2;
+    if (const char* ev = getenv("GD_MSDA_SORTED_F")) {  // A/B: fixed split for every level
+      const int f = atoi(ev);
+      if (f >= 1 && f <= maxF && (f & (f - 1)) == 0) F = f;
+    }
+    G.F[l] = F;
+    G.bstart[l] = int(bl);
+    bl += (int64_t(N) * G.H[l] * G.W[l] * M * F + gpb - 1) / gpb;
+  }
+  if (bl >= (int64_t(1) << 31)) return false;
+  G.bstart[4] = int(bl);
+  pl.ncells = int(ncells);
+  pl.nsamples = int(units * 16);
+  pl.nb = int((ncells + kScanBlock - 1) / kScanBlock);
+  if (pl.nb > 256 * kScanPer) return false;
+  const int upb = 4 * (64 / lpu);  // units per K1 block
+  pl.k1_blocks = int((units + upb - 1) / upb);
+  size_t o = 0;
+  pl.o_cnt = o; o = align_up(o + sizeof(int) * size_t(ncells));        // counts, then scatter cursor
+  pl.o_off = o; o = align_up(o + sizeof(int) * size_t(ncells + 1));    // segment offsets
+  pl.o_bsum = o; o = align_up(o + sizeof(int) * size_t(pl.nb));
+  pl.o_ids = o; o = align_up(o + sizeof(int) * size_t(pl.nsamples));   // sample ids by cell
+  pl.o_scr = o;
+  if (flags & GD_MSDA_DETERMINISTIC) o = align_up(o + sizeof(int) * size_t(pl.nsamples));
+  pl.bytes = o;
+  return true;
+}
+
+}  // namespace
+}  // namespace gd
+
+extern "C" size_t gd_msda_backward_workspace_bytes(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P,
+                                                   const int64_t* shapes_host, int flags) {
+  SortedPlan pl;
+  return plan_sorted(dt, N, S, M, D, L, Lq, P, shapes_host, flags, pl) ? pl.bytes : 0;
+}
+
+extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, const int64_t* shapes,
+                                             const int64_t* lsi, const void* loc, const void* attn,
+                                             const void* grad_out, int N, int S, int M, int D, int L, int Lq,
+                                             int P, void* grad_value, gd_dtype gv_dt, void* grad_loc,
+                                             void* grad_attn, const int64_t* shapes_host, void* ws,
+                                             size_t ws_bytes, int flags, gd_stream_t stream) {
+  gd_status st0 = check_common(dt, N, S, M, D, L, Lq, P);
+  if (st0 != GD_OK) return st0;
+  (void)shapes;
+  (void)lsi;  // the level geometry comes from the host shapes (lsi = their cumulative sums)
+  SortedPlan pl;
+  if (!plan_sorted(dt, N, S, M, D, L, Lq, P, shapes_host, flags, pl)) {
+    set_error("msda_backward_sorted: not applicable (value F32/BF16, D=32, L=P=4, host shapes tiling "
+              "spatial_size, 32-bit offsets)");
+    return GD_ERR_UNSUPPORTED;
+  }
+  GD_REQUIRE(gv_dt == GD_F32 || (gv_dt == GD_BF16 && dt == GD_BF16),
+             "msda_backward_sorted: grad_value dtype %d (F32, or BF16 for a BF16 value)", int(gv_dt));
+  GD_REQUIRE(ws && ws_bytes >= pl.bytes, "msda_backward_sorted: workspace of %zu bytes needed", pl.bytes);
+  GD_REQUIRE(grad_value && (Lq == 0 || (value && loc && attn && grad_out && grad_loc && grad_attn)),
+             "msda_backward_sorted: null pointer");
+  GD_REQUIRE(aligned16(value) && aligned16(loc) && aligned16(attn) && aligned16(grad_out) && aligned16(grad_loc) &&
+                 aligned16(grad_attn) && aligned16(grad_value),
+             "msda_backward_sorted: operands must be 16-byte aligned");
+  hipStream_t s = as_hip(stream);
+  char* w = static_cast<char*>(ws);
+  int* cnt = reinterpret_cast<int*>(w + pl.o_cnt);
+  int* off = reinterpret_cast<int*>(w + pl.o_off);
+  int* bsum = reinterpret_cast<int*>(w + pl.o_bsum);
+  int* ids = reinterpret_cast<int*>(w + pl.o_ids);
+  int* scr = reinterpret_cast<int*>(w + pl.o_scr);
+  const int units = pl.nsamples / 16;
+  GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells), s));
+  if (units > 0) {
+    if (dt == GD_BF16)
+      hipLaunchKernelGGL((msda_bwd_samples<uint16_t>), dim3(pl.k1_blocks), dim3(256), 0, s, (const uint16_t*)value,
+                         (const float*)loc, (const float*)attn, (const uint16_t*)grad_out, (float*)grad_loc,
+                         (float*)grad_attn, cnt, pl.G, S, Lq, M, units);
+    else
+      hipLaunchKernelGGL((msda_bwd_samples<float>), dim3(pl.k1_blocks), dim3(256), 0, s, (const float*)value,
+                         (const float*)loc, (const float*)attn, (const float*)grad_out, (float*)grad_loc,
+                         (float*)grad_attn, cnt, pl.G, S, Lq, M, units);
+    GD_LAUNCH_CHECK("msda_bwd_samples");
+  }
+  hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);
+  hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(256), 0, s, bsum, pl.nb);
+  hipLaunchKernelGGL(scan_finish, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, (const int*)bsum, off,
+                     cnt);
+  GD_LAUNCH_CHECK("msda_bwd scan");
+  if (units > 0) {
+    hipLaunchKernelGGL(msda_bwd_scatter, dim3((pl.nsamples + 255) / 256), dim3(256), 0, s, (const float*)loc, cnt,
+                       ids, pl.G, Lq, M, pl.nsamples);
+    GD_LAUNCH_CHECK("msda_bwd_scatter");
+    if (flags & GD_MSDA_DETERMINISTIC) {
+      int bits = 1;
+      while (bits < 31 && (int64_t(1) << bits) < pl.nsamples) ++bits;
+      hipLaunchKernelGGL(msda_bwd_sort_cells, dim3((pl.ncells + 3) / 4), dim3(256), 0, s, (const int*)off, ids, scr,
+                         pl.ncells, bits);
+      GD_LAUNCH_CHECK("msda_bwd_sort_cells");
+    }
+  }
+#define GD_K4(T, TO)                                                                                            \
+  hipLaunchKernelGGL((msda_bwd_value<T, TO>), dim3(pl.G.bstart[4]), dim3(256), 0, s, (const T*)grad_out,        \
+                     (const float*)loc, (const float*)attn, (const int*)off, (const int*)ids, (TO*)grad_value, pl.G, \
+                     S, M)
+  if (dt == GD_BF16 && gv_dt == GD_BF16) GD_K4(uint16_t, uint16_t);
+  else if (dt == GD_BF16) GD_K4(uint16_t, float);
+  else GD_K4(float, float);
+#undef GD_K4
+  GD_LAUNCH_CHECK("msda_bwd_value");
+  return GD_OK;
 }

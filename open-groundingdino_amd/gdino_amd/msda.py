@@ -19,10 +19,35 @@ fp32), and launch errors raise instead of being printed.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib
+
+_p, _i = ctypes.c_void_p, ctypes.c_int
+_lib.register("gd_msda_backward_sorted", [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 +
+              [_p, _i, _p, _p, _p, _p, ctypes.c_size_t, _i, _p])
+GD_MSDA_DETERMINISTIC = 1
+
+
+def _workspace_bytes(dt, N, S, M, D, L, Lq, P, hs, flags) -> int:
+    fn = _lib.lib().gd_msda_backward_workspace_bytes
+    fn.restype = ctypes.c_size_t
+    fn.argtypes = [_i] * 8 + [_p, _i]
+    return int(fn(dt, N, S, M, D, L, Lq, P, hs, flags))
+
+
+def deterministic() -> bool:
+    """Deterministic MSDA backward (GD_MSDA_DETERMINISTIC flag of the sorted
+    kernel): torch.use_deterministic_algorithms(True) or GD_MSDA_DETERMINISTIC=1."""
+    return torch.are_deterministic_algorithms_enabled() or os.environ.get("GD_MSDA_DETERMINISTIC") == "1"
+
+
+def backward_variant() -> str:
+    """GD_MSDA_BWD: sorted (default: atomic-free, csrc/msda_sorted.inc), or
+    the round-1/2 kernels for A/B runs: enc / lane32 / tiled."""
+    return os.environ.get("GD_MSDA_BWD", "sorted")
 
 
 class LaunchTimer:
@@ -57,13 +82,15 @@ class LaunchTimer:
 timer = None  # set to a LaunchTimer to measure
 
 
-def algorithmic_bytes(kind, N, S, M, D, L, Lq, P, sv, sf=4, so=None):
+def algorithmic_bytes(kind, N, S, M, D, L, Lq, P, sv, sf=4, so=None, sg=4):
     """SURVEY §8d per-launch algorithmic traffic.  fwd: value + (loc, attn) +
-    out.  bwd: value + grad_value (fp32) + 2x(loc, attn, grads) + grad_out."""
+    out.  bwd: value + grad_value (sg bytes per element: fp32 for the atomic
+    kernels' accumulation buffer, the value dtype when the sorted kernel
+    writes it directly) + 2x(loc, attn, grads) + grad_out."""
     so = sv if so is None else so
     if kind == "fwd":
         return sv * N * S * M * D + 3 * sf * N * Lq * M * L * P + so * N * Lq * M * D
-    return sv * N * S * M * D + 4 * N * S * M * D + 6 * sf * N * Lq * M * L * P + so * N * Lq * M * D
+    return sv * N * S * M * D + sg * N * S * M * D + 6 * sf * N * Lq * M * L * P + so * N * Lq * M * D
 
 
 def _acc_dtype(value: torch.Tensor) -> torch.dtype:
@@ -154,6 +181,14 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     if grad_output.numel() != N * Lq * M * D:
         raise RuntimeError("grad_output must be [N, Lq, M*D]")
     acc = _acc_dtype(value)
+    hs = None
+    if host_shapes is not None and len(host_shapes) == L:
+        hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
+    if value.is_cuda and hs is not None and backward_variant() in ("sorted", "auto"):
+        out = _backward_sorted(value, spatial_shapes, level_start_index, loc, attn, grad_output,
+                               (N, S, M, D, L, Lq, P), hs, grad_value_dtype)
+        if out is not None:
+            return _finish_grads(value, sampling_loc, attn_weight, *out, grad_value_dtype)
     grad_value = torch.empty((N, S, M, D), dtype=acc, device=value.device)
     grad_loc = torch.empty((N, Lq, M, L, P, 2), dtype=acc, device=value.device)
     grad_attn = torch.empty((N, Lq, M, L, P), dtype=acc, device=value.device)
@@ -162,9 +197,6 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
                       level_start_index.data_ptr(), loc.data_ptr(), attn.data_ptr(), grad_output.data_ptr(),
                       N, S, M, D, L, Lq, P, grad_value.data_ptr(), grad_loc.data_ptr(), grad_attn.data_ptr(), None)
         return _finish_grads(value, sampling_loc, attn_weight, grad_value, grad_loc, grad_attn, grad_value_dtype)
-    hs = None
-    if host_shapes is not None and len(host_shapes) == L:
-        hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
     nbytes = algorithmic_bytes("bwd", N, S, M, D, L, Lq, P, value.element_size())
     t0 = timer.begin() if timer is not None else None
     _lib.call("gd_msda_backward_geom", _lib.dtype_code(value), value.data_ptr(), spatial_shapes.data_ptr(),
@@ -174,6 +206,35 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     if t0 is not None:
         timer.end("bwd", Lq, nbytes, t0)
     return _finish_grads(value, sampling_loc, attn_weight, grad_value, grad_loc, grad_attn, grad_value_dtype)
+
+
+def _backward_sorted(value, shapes, lsi, loc, attn, grad_output, dims, hs, grad_value_dtype):
+    """gd_msda_backward_sorted (no float atomics; bitwise deterministic when
+    deterministic()): grad_value written once per row, directly in
+    grad_value_dtype when that is value.dtype or fp32.  None when the kernel
+    does not apply to these sizes (the caller then runs gd_msda_backward_geom)."""
+    N, S, M, D, L, Lq, P = dims
+    out_dtype = value.dtype if grad_value_dtype is None else grad_value_dtype
+    if out_dtype not in (value.dtype, torch.float32):
+        return None
+    flags = GD_MSDA_DETERMINISTIC if deterministic() else 0
+    dt = _lib.dtype_code(value)
+    nws = _workspace_bytes(dt, N, S, M, D, L, Lq, P, hs, flags)
+    if nws == 0:
+        return None
+    ws = torch.empty(nws, dtype=torch.uint8, device=value.device)
+    grad_value = torch.empty((N, S, M, D), dtype=out_dtype, device=value.device)
+    grad_loc = torch.empty((N, Lq, M, L, P, 2), dtype=torch.float32, device=value.device)
+    grad_attn = torch.empty((N, Lq, M, L, P), dtype=torch.float32, device=value.device)
+    nbytes = algorithmic_bytes("bwd", N, S, M, D, L, Lq, P, value.element_size(), sg=grad_value.element_size())
+    t0 = timer.begin() if timer is not None else None
+    _lib.call("gd_msda_backward_sorted", dt, value.data_ptr(), shapes.data_ptr(), lsi.data_ptr(), loc.data_ptr(),
+              attn.data_ptr(), grad_output.data_ptr(), N, S, M, D, L, Lq, P, grad_value.data_ptr(),
+              _lib.dtype_code(grad_value), grad_loc.data_ptr(), grad_attn.data_ptr(), hs, ws.data_ptr(), nws, flags,
+              _lib.stream_of(value), nbytes=nbytes)
+    if t0 is not None:
+        timer.end("bwd", Lq, nbytes, t0)
+    return [grad_value, grad_loc, grad_attn]
 
 
 def _finish_grads(value, sampling_loc, attn_weight, grad_value, grad_loc, grad_attn, grad_value_dtype):

@@ -48,20 +48,43 @@ def synthetic_caption(rng: random.Random, n_tokens: int = 256) -> List[str]:
     return phrases
 
 
+def synthetic_grounding(rng: random.Random, n_boxes: int, n_phrases: int = 6) -> Tuple[List[str], List[int]]:
+    """VG-style regions (datasets/odvg.py:236-252): free-text phrases of 2-6
+    words, several boxes sharing a phrase; the caption is the unique phrases
+    (first-occurrence order) and a box's label indexes its phrase.
+    -> (unique phrases, label per box)."""
+    used: set = set()
+    n_uniq = max(1, min(n_phrases, (n_boxes + 1) // 2))  # boxes share phrases
+    pool = [_phrase_words(rng, rng.randint(2, 6), used) for _ in range(n_uniq)]
+    phrases = [pool[i % len(pool)] for i in range(n_boxes)]  # every phrase used, some repeated
+    rng.shuffle(phrases)
+    uniq = list(dict.fromkeys(phrases))
+    index = {p: i for i, p in enumerate(uniq)}
+    return uniq, [index[p] for p in phrases]
+
+
 def synthetic_batch(bs: int, height: int, width: int, n_boxes: int = 8, n_tokens: int = 256, seed: int = 0,
-                    device="cuda", dtype=torch.float32) -> Tuple[NestedTensor, list, list, list]:
+                    device="cuda", dtype=torch.float32, vg_images: int = 0) -> Tuple[NestedTensor, list, list, list]:
     """-> (samples, targets, captions, cat_lists) shaped like an odvg batch
     (datasets/odvg.py:254-260): boxes cxcywh normalised (centres U[0.2,0.8],
-    sizes U[0.05,0.3]), labels index the image's phrase list."""
+    sizes U[0.05,0.3]), labels index the image's phrase list.  The first
+    bs - vg_images images are OD-style (category-name captions of n_tokens
+    tokens); the last vg_images are VG-style grounding samples
+    (synthetic_grounding: a short caption of unique free-text phrases, boxes
+    sharing phrases) -- BASELINE config 5's mixed OD+VG batch."""
     rng = random.Random(seed)
     g = torch.Generator().manual_seed(seed)
     imgs = torch.randn(bs, 3, height, width, generator=g).to(device, dtype)
     mask = torch.zeros(bs, height, width, dtype=torch.bool, device=device)
     targets, captions, cat_lists = [], [], []
     for i in range(bs):
-        cats = synthetic_caption(rng, n_tokens)
+        if i >= bs - vg_images:
+            cats, vg_labels = synthetic_grounding(rng, n_boxes)
+            labels = torch.as_tensor(vg_labels, dtype=torch.int64)
+        else:
+            cats = synthetic_caption(rng, n_tokens)
+            labels = torch.randint(0, len(cats), (n_boxes,), generator=g)
         caption = " . ".join(cats) + " ."
-        labels = torch.randint(0, len(cats), (n_boxes,), generator=g)
         ctr = torch.rand(n_boxes, 2, generator=g) * 0.6 + 0.2
         wh = torch.rand(n_boxes, 2, generator=g) * 0.25 + 0.05
         boxes = torch.cat([ctr, wh], -1)

@@ -34,11 +34,13 @@ class MSDeformAttnFunction(Function):
     @once_differentiable
     def backward(ctx, grad_output):
         value, shapes, lsi, loc, attn = ctx.saved_tensors
-        # grad_value stays in its fp32 accumulation buffer; autograd casts it
-        # to value.dtype if they differ (one pass either way).
+        # the sorted backward writes grad_value in value.dtype directly; the
+        # atomic kernels keep their fp32 accumulation buffer, which autograd
+        # casts to value.dtype (one pass either way)
         grad_value, grad_loc, grad_attn = MSDA.ms_deform_attn_backward(
             value, shapes, lsi, loc, attn, grad_output.contiguous(), ctx.im2col_step,
-            grad_value_dtype=torch.float64 if value.dtype == torch.float64 else torch.float32,
+            grad_value_dtype=value.dtype if value.dtype == torch.bfloat16 else
+            (torch.float64 if value.dtype == torch.float64 else torch.float32),
             host_shapes=ctx.host_shapes)
         return grad_value, None, None, grad_loc, grad_attn, None
 

@@ -248,6 +248,16 @@ inline void wave_gather(const void* mine, size_t nbytes, void* all) {
   }
 }
 
+// __ballot: bit i = predicate of lane i (all 64 lanes of the wave take part)
+inline unsigned long long ballot(int pred) {
+  const uint8_t mine = pred ? 1 : 0;
+  uint8_t all[64];
+  wave_gather(&mine, 1, all);
+  unsigned long long m = 0;
+  for (unsigned i = 0; i < 64; ++i) m |= (unsigned long long)(all[i] & 1u) << i;
+  return m;
+}
+
 // ds_read_b64_tr_b16 (gfx950): per 16-lane group, lane 4q+p supplies the
 // address of row q, columns 4p..4p+3 of a 4 x 16 block of 16-bit elements;
 // lane i receives column i of the 4 rows (row q in element q)
@@ -329,6 +339,9 @@ void launch(dim3 g, dim3 b, F&& f) {
 #define gridDim (::gd_emu::grid().grid)
 #define blockDim (::gd_emu::grid().block)
 #define __syncthreads() ::gd_emu::syncthreads()
+#define __ballot(pred) ::gd_emu::ballot(pred)
+#define __threadfence() ((void)0)  // one OS thread: memory is coherent
+inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 #define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
 #define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
 // compiler scheduling hints: no semantics to emulate

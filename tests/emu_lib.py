@@ -30,6 +30,10 @@ def lib():
         _LIB.gd_msda_forward.argtypes = [_i, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p]
         _LIB.gd_msda_backward.argtypes = [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p, _p, _p]
         _LIB.gd_msda_backward_geom.argtypes = [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p, _p, _p, _p]
+        _LIB.gd_msda_backward_workspace_bytes.argtypes = [_i] * 8 + [_p, _i]
+        _LIB.gd_msda_backward_workspace_bytes.restype = ctypes.c_size_t
+        _LIB.gd_msda_backward_sorted.argtypes = ([_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 +
+                                                 [_p, _i, _p, _p, _p, _p, ctypes.c_size_t, _i, _p])
         _LIB.gd_biattn_workspace_bytes.argtypes = [_i] * 4
         _LIB.gd_biattn_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_biattn_softmax_fwd.argtypes = [_i, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p]
@@ -103,6 +107,29 @@ def msda_backward(value, shapes, lsi, loc, attn, grad_out, host_shapes=None):
         _check(lib().gd_msda_backward_geom(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc),
                                            _ptr(attn), _ptr(grad_out), N, S, M, D, L, Lq, P, _ptr(gv), _ptr(gl),
                                            _ptr(ga), hs, None))
+    return gv, gl, ga
+
+
+def msda_backward_sorted(value, shapes, lsi, loc, attn, grad_out, host_shapes, gv_dtype=torch.float32,
+                         deterministic=False):
+    """gd_msda_backward_sorted -> grad_value (gv_dtype), grad_loc, grad_attn
+    (f32); None when the sorted backward does not apply."""
+    N, S, M, D = value.shape
+    _, Lq, _, L, P, _ = loc.shape
+    value, loc, attn, grad_out = (t.contiguous() for t in (value, loc, attn, grad_out))
+    shapes, lsi = shapes.to(torch.int64).contiguous(), lsi.to(torch.int64).contiguous()
+    hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
+    flags = 1 if deterministic else 0
+    nb = lib().gd_msda_backward_workspace_bytes(_code(value), N, S, M, D, L, Lq, P, hs, flags)
+    if nb == 0:
+        return None
+    ws = torch.empty(nb, dtype=torch.uint8)
+    gv = torch.full((N, S, M, D), float("nan"), dtype=gv_dtype)  # every row must be written
+    gl = torch.full((N, Lq, M, L, P, 2), float("nan"), dtype=torch.float32)
+    ga = torch.full((N, Lq, M, L, P), float("nan"), dtype=torch.float32)
+    _check(lib().gd_msda_backward_sorted(_code(value), _ptr(value), _ptr(shapes), _ptr(lsi), _ptr(loc), _ptr(attn),
+                                         _ptr(grad_out), N, S, M, D, L, Lq, P, _ptr(gv), _code(gv), _ptr(gl),
+                                         _ptr(ga), hs, _ptr(ws), nb, flags, None))
     return gv, gl, ga
 
 

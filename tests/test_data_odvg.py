@@ -157,3 +157,59 @@ def test_model_step_from_loader(odvg_dir):
         loss.backward()
     assert torch.isfinite(loss)
     assert model.transformer.level_embed.grad is not None
+
+
+# ------------------------------------------- pinned to the reference (round 3)
+def _ref_cases():
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "odvg_ref.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def ref_odvg_dir(tmp_path_factory):
+    """The fixture's images (tests/golden/make_odvg_golden.py write_images)."""
+    d = tmp_path_factory.mktemp("odvg_ref")
+    rng = np.random.default_rng(0)
+    for i in range(3):
+        Image.fromarray(rng.integers(0, 255, (40, 48, 3), dtype=np.uint8)).save(d / f"img{i}.png")
+    return d
+
+
+def test_odvg_matches_reference_golden(ref_odvg_dir):
+    """Every OD / VG case of tests/golden/odvg_ref.json (the reference's own
+    ODVGDataset.__getitem__, global `random` seeded per case): same RNG draws
+    -> same negatives, same shuffles, same boxes in the same order, every
+    box's label naming its category / phrase.  The reference orders OD
+    positives and VG unique phrases by list(set(...)) (string-hash order,
+    PYTHONHASHSEED=0 in the fixture); the product uses sorted / first
+    occurrence order, so those lists compare as sets -- and exactly when the
+    order cannot differ (one distinct positive label)."""
+    import random as pyrandom
+
+    from gdino_amd.data import ODVGDataset
+    gold = _ref_cases()
+    (ref_odvg_dir / "label_map.json").write_text(json.dumps(gold["label_map"]))
+    n_exact = 0
+    for i, case in enumerate(gold["cases"]):
+        meta, out = case["meta"], case["out"]
+        anno = ref_odvg_dir / f"case{i}.jsonl"
+        anno.write_text(json.dumps(meta) + "\n")
+        lm = str(ref_odvg_dir / "label_map.json") if case["mode"] == "OD" else None
+        ds = ODVGDataset(str(ref_odvg_dir), str(anno), lm, max_labels=case["max_labels"])
+        pyrandom.seed(case["seed"])
+        _, t = ds[0]
+        cap, labels = t["cap_list"], t["labels"].tolist()
+        assert t["caption"] == " . ".join(cap) + " ."
+        assert set(cap) == set(out["cap_list"]) and len(cap) == len(out["cap_list"]), (i, cap, out["cap_list"])
+        ref_names = [out["cap_list"][j] for j in out["labels"]]
+        assert [cap[j] for j in labels] == ref_names, i  # each box names the same category / phrase
+        assert t["boxes"].tolist() == out["boxes"], i    # same boxes in the same (shuffled) order
+        if case["mode"] == "OD":
+            n_pos = len({o["label"] for o in meta["detection"]["instances"]})
+            if n_pos == 1:
+                assert cap == out["cap_list"], i
+                n_exact += 1
+        else:
+            assert out.get("fork_vg_raises")  # the fork's VG branch crashes after computing these
+    assert n_exact >= 4

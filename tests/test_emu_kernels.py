@@ -107,6 +107,63 @@ def test_emulated_forward_nonfinite_locations_add_zero(vdtype):
     assert E.rel_err(out.double(), ref) < (1e-5 if vdtype == torch.float32 else 1e-2)
 
 
+# ------------------------------- sorted backward (no float atomics, round 3)
+def _check_sorted(inputs, levels, tol, gv_dtype=torch.float32, deterministic=False):
+    from msda_cases import rel_err_grad_loc
+    res = E.msda_backward_sorted(*inputs, host_shapes=levels, gv_dtype=gv_dtype, deterministic=deterministic)
+    assert res is not None
+    gv, gl, ga = res
+    assert torch.isfinite(gv).all() and torch.isfinite(gl).all() and torch.isfinite(ga).all()
+    rgv, rgl, rga = _oracle_bwd(*inputs)
+    assert E.rel_err(gv.double(), rgv) < (tol if gv_dtype == torch.float32 else 1e-2)
+    assert rel_err_grad_loc(gl, rgl, inputs[3], inputs[1]) < tol  # away from cell edges
+    assert E.rel_err(ga, rga) < tol
+    return gv, gl, ga
+
+
+@pytest.mark.parametrize("levels,n,lq,local,outliers,vdtype", [
+    (SMALL, 1, None, True, 0.0, torch.float32),      # encoder shape, Lq == S
+    (MEDIUM, 2, None, True, 0.1, torch.float32),     # + outliers, batch of 2
+    (MEDIUM, 2, None, True, 0.05, torch.bfloat16),   # bf16 value / grad_out
+    (MEDIUM, 2, 37, False, 0.0, torch.float32),      # decoder shape: Lq != S, points anywhere (and outside)
+    (WIDE, 1, 23, False, 0.0, torch.bfloat16),
+])
+def test_emulated_sorted_backward_matches_oracle(levels, n, lq, local, outliers, vdtype):
+    S = sum(h * w for h, w in levels)
+    inputs = _levels_inputs(levels, n, S if lq is None else lq, seed=11, vdtype=vdtype, local=local,
+                            outlier_frac=outliers)
+    _check_sorted(inputs, levels, 1e-5)
+
+
+def test_emulated_sorted_backward_bf16_grad_value_and_determinism():
+    """grad_value written directly in bf16 (the autograd dtype of a bf16
+    value) equals the fp32 result rounded; the deterministic mode sorts each
+    cell segment by sample id, so two runs agree bit for bit, and the sums
+    agree with the arrival-order mode to fp32 rounding."""
+    inputs = _levels_inputs(MEDIUM, 2, 380, seed=12, vdtype=torch.bfloat16, local=True, outlier_frac=0.1)
+    gv32, gl, ga = _check_sorted(inputs, MEDIUM, 1e-5)
+    gv16, gl2, ga2 = _check_sorted(inputs, MEDIUM, 1e-5, gv_dtype=torch.bfloat16)
+    assert torch.equal(gv16, gv32.to(torch.bfloat16))
+    assert torch.equal(gl, gl2) and torch.equal(ga, ga2)  # no atomics in grad_loc / grad_attn
+    d1 = _check_sorted(inputs, MEDIUM, 1e-5, deterministic=True)
+    d2 = _check_sorted(inputs, MEDIUM, 1e-5, deterministic=True)
+    for a, b in zip(d1, d2):
+        assert torch.equal(a, b)
+    assert E.rel_err(d1[0].double(), gv32.double().numpy()) < 1e-6
+
+
+def test_emulated_sorted_backward_long_cell_segments():
+    """Cells holding > 64 samples take the deterministic mode's wave radix
+    sort (not the register bitonic): every query samples the same few
+    points."""
+    levels = [(3, 4), (2, 2), (1, 2), (1, 1)]
+    S = sum(h * w for h, w in levels)
+    value, shapes, lsi, loc, attn, grad_out = _levels_inputs(levels, 1, 90, seed=13)
+    g = torch.Generator().manual_seed(3)
+    loc = (torch.rand(1, 90, 8, 4, 4, 2, generator=g) * 0.05 + 0.3)  # all in one cell per level
+    _check_sorted((value, shapes, lsi, loc, attn, grad_out), levels, 1e-5, deterministic=True)
+
+
 # ------------------------------------------- tiled (LDS) encoder backward
 @pytest.mark.parametrize("levels,n,local,outliers", [
     (SMALL, 1, False, 0.0),     # every level box fits: all-LDS path

@@ -270,8 +270,6 @@ def test_cast_cache_follows_fused_adamw_updates(built):
     counters; the cast cache must still serve the updated weights on the next
     step.  Two train steps with the cache on and off (fp32-exact casts: same
     bits) must give bit-identical second-step losses."""
-    import copy
-
     from gdino_amd import castcache
     from gdino_amd.train import synthetic_batch, train_step
     args, model0, criterion, *_ = built
@@ -283,11 +281,15 @@ def test_cast_cache_follows_fused_adamw_updates(built):
     opt.step()
     assert p._version == v, "fused AdamW bumps versions now: the generation guard is still needed for foreach=False"
     losses = {}
+    model = model0
+    state = {k: v.clone() for k, v in model.state_dict().items()}
+    drop = {id(m): (m.p if isinstance(m, torch.nn.Dropout) else m.drop_prob) for m in model.modules()
+            if isinstance(m, torch.nn.Dropout) or hasattr(m, "drop_prob")}
     for enabled in (True, False):
         castcache.ENABLED = enabled
         castcache.FUSE_SHARED_INPUT = False  # same GEMMs both ways (bit-identical gradients)
         castcache.clear()
-        model = copy.deepcopy(model0)
+        model.load_state_dict(state)
         model.train()
         for m in model.modules():  # deterministic: no dropout / drop-path
             if isinstance(m, torch.nn.Dropout):
@@ -303,6 +305,35 @@ def test_cast_cache_follows_fused_adamw_updates(built):
             castcache.ENABLED = True
             castcache.FUSE_SHARED_INPUT = True
             castcache.clear()
+            model.load_state_dict(state)
+            model.zero_grad(set_to_none=True)
+            for m in model.modules():
+                if id(m) in drop:
+                    if isinstance(m, torch.nn.Dropout):
+                        m.p = drop[id(m)]
+                    else:
+                        m.drop_prob = drop[id(m)]
     assert losses[True][0] == losses[False][0]
     assert losses[True][1] == losses[False][1], losses
     assert losses[True][1] != losses[True][0]
+
+
+def test_mixed_od_vg_batch_trains(built):
+    """BASELINE config 5's mixed batch: one OD image (category-name caption)
+    and one VG image (short caption of unique free-text phrases, several boxes
+    per phrase, datasets/odvg.py:236-252) through one train step on the
+    product's host logic (HIP-only ops routed to the oracle)."""
+    from gdino_amd.train import synthetic_batch, train_step
+    args, model, criterion, *_ = built
+    samples, targets, caps, cats = synthetic_batch(2, 128, 160, n_boxes=5, n_tokens=40, seed=3, device="cpu",
+                                                   vg_images=1)
+    od, vg = targets
+    assert len(cats[0]) > len(cats[1]) >= 1 and len(set(cats[1])) == len(cats[1])
+    assert all(len(p.split()) >= 2 for p in cats[1])           # free-text phrases
+    assert len(set(vg["labels"].tolist())) == len(cats[1]) < 5  # phrases shared by boxes, all used
+    assert vg["caption"] == " . ".join(cats[1]) + " ."
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-5)
+    model.train()
+    with oracle_msda():
+        loss = train_step(model, criterion, opt, samples, targets, caps, cats)
+    assert torch.isfinite(loss)

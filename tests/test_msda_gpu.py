@@ -242,7 +242,7 @@ def test_encoder_tiled_backward_800x1333(vdtype, tol, monkeypatch):
 
 
 @pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("variant", ["tiled", "auto", "enc"])
+@pytest.mark.parametrize("variant", ["tiled", "auto", "enc", "sorted"])
 def test_encoder_pixel_block_backward_800x1333(vdtype, tol, variant, monkeypatch):
     """gd_msda_backward_geom (host level shapes -> 4 x 8 pixel-block tiles
     with GD_MSDA_BWD=tiled), the path the model's encoder takes."""
@@ -252,7 +252,7 @@ def test_encoder_pixel_block_backward_800x1333(vdtype, tol, variant, monkeypatch
 
 
 @pytest.mark.parametrize("levels", [[(6, 9), (3, 5), (2, 3), (1, 2)], [(13, 21), (7, 11), (4, 6), (2, 3)]])
-@pytest.mark.parametrize("variant", ["tiled", "enc"])
+@pytest.mark.parametrize("variant", ["tiled", "enc", "sorted"])
 def test_encoder_pixel_block_backward_small(levels, variant, monkeypatch):
     monkeypatch.setenv("GD_MSDA_BWD", variant)
     _check_bwd_vs_oracle(_encoder_inputs(levels, 2, seed=3, vdtype=torch.float32, outlier_frac=0.05), 1e-3,
@@ -320,7 +320,7 @@ def _init_geometry_loc(levels, n):
     return loc[None].expand(n, -1, -1, -1, -1, -1).contiguous()
 
 
-@pytest.mark.parametrize("variant", ["lane32", "tiled", "enc"])
+@pytest.mark.parametrize("variant", ["lane32", "tiled", "enc", "sorted"])
 @pytest.mark.parametrize("vdtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
 def test_encoder_backward_init_geometry_800x1333(variant, vdtype, tol, monkeypatch):
     """Sampling points on cell edges (the reference init): a kernel that
@@ -345,6 +345,70 @@ def test_encoder_enc_matches_direct_atomic_kernel(vdtype, monkeypatch):
     # grad_attn: per-lane dot products summed in a different order
     torch.testing.assert_close(enc[2], direct[2], rtol=1e-4, atol=1e-5)
     assert _rel_err_gl(enc[1].cpu(), direct[1].double().cpu().numpy(), inputs[3].cpu(), inputs[1].cpu()) < 1e-5
+
+
+# ------------------------------ sorted backward (no float atomics, round 3)
+@pytest.mark.parametrize("lq,vdtype,tol", [(900, torch.float32, 1e-3), (900, torch.bfloat16, 1e-2)])
+def test_sorted_backward_decoder_shape_800x1333(lq, vdtype, tol, monkeypatch):
+    """The decoder's cross-attention (900 queries sampling anywhere, also
+    outside the levels) through the sorted backward (host shapes given, as the
+    model passes them)."""
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    value, shapes, lsi, loc, attn, grad_out = _big_inputs(lq, seed=lq + 1, vdtype=vdtype)
+    inputs = (value.cpu(), shapes, lsi, loc.cpu(), attn.cpu(), grad_out.cpu())
+    _check_bwd_vs_oracle(inputs, tol, host_shapes=LEVELS_800)
+
+
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+def test_sorted_matches_direct_atomic_kernel(vdtype, monkeypatch):
+    """Same sums, different order: the destination-sorted backward against
+    msda_bwd_lane32 (float atomics) on one encoder-shape input."""
+    inputs = [t.to(DEV) for t in _encoder_inputs(LEVELS_800, 2, seed=17, vdtype=vdtype, outlier_frac=0.02)]
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    srt = _msda().ms_deform_attn_backward(*inputs, 64, grad_value_dtype=torch.float32, host_shapes=LEVELS_800)
+    monkeypatch.setenv("GD_MSDA_BWD", "lane32")
+    direct = _msda().ms_deform_attn_backward(*inputs, 64, grad_value_dtype=torch.float32, host_shapes=LEVELS_800)
+    torch.testing.assert_close(srt[0], direct[0], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(srt[2], direct[2], rtol=1e-4, atol=1e-5)
+    assert _rel_err_gl(srt[1].cpu(), direct[1].double().cpu().numpy(), inputs[3].cpu(), inputs[1].cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("lq", [22223, 900])
+def test_sorted_backward_deterministic_mode_is_bitwise_reproducible(lq, monkeypatch):
+    """GD_MSDA_DETERMINISTIC=1 (or torch.use_deterministic_algorithms): each
+    cell's sample list is sorted by sample id before the per-destination sums,
+    so two runs give bitwise-equal grad_value (and grad_loc / grad_attn, which
+    never use atomics).  bf16 value, grad_value written in bf16 as autograd
+    takes it."""
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "1")
+    if lq == 900:
+        inputs = [t.to(DEV) for t in _big_inputs(900, seed=5, vdtype=torch.bfloat16)]
+    else:
+        inputs = [t.to(DEV) for t in _encoder_inputs(LEVELS_800, 2, seed=19, vdtype=torch.bfloat16,
+                                                     outlier_frac=0.02)]
+    runs = [_msda().ms_deform_attn_backward(*inputs, 64, host_shapes=LEVELS_800) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert runs[0][0].dtype == torch.bfloat16
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "0")
+    fast = _msda().ms_deform_attn_backward(*inputs, 64, host_shapes=LEVELS_800)
+    torch.testing.assert_close(fast[0].float(), runs[0][0].float(), rtol=1e-2, atol=1e-3)
+    assert torch.equal(fast[1], runs[0][1]) and torch.equal(fast[2], runs[0][2])
+
+
+def test_sorted_backward_bf16_grad_value_is_the_rounded_fp32_sum(monkeypatch):
+    """grad_value in bf16 straight from the kernel equals the kernel's fp32
+    result rounded to bf16 (same sums, deterministic mode)."""
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "1")
+    inputs = [t.to(DEV) for t in _encoder_inputs(LEVELS_800, 2, seed=23, vdtype=torch.bfloat16)]
+    g16 = _msda().ms_deform_attn_backward(*inputs, 64, grad_value_dtype=torch.bfloat16, host_shapes=LEVELS_800)
+    g32 = _msda().ms_deform_attn_backward(*inputs, 64, grad_value_dtype=torch.float32, host_shapes=LEVELS_800)
+    assert g16[0].dtype == torch.bfloat16 and g32[0].dtype == torch.float32
+    assert torch.equal(g16[0], g32[0].to(torch.bfloat16))
 
 
 # ------------------------------------------------------------- edge/contract

@@ -189,6 +189,50 @@ def fwd_variants(iters):
             os.environ.pop("GD_MSDA_FWD_SB", None)
 
 
+BWD_VARIANTS = [
+    ("sorted", {"GD_MSDA_BWD": "sorted"}),
+    ("sorted deterministic", {"GD_MSDA_BWD": "sorted", "GD_MSDA_DETERMINISTIC": "1"}),
+    ("enc", {"GD_MSDA_BWD": "enc"}),
+    ("lane32", {"GD_MSDA_BWD": "lane32"}),
+]
+
+
+def bwd_variants(iters):
+    """The backward as the model calls it (bf16 value, host level shapes,
+    grad_value returned in bf16) under each kernel, encoder shape at the init
+    geometry and a 2-px spread, and the decoder shape; checked against lane32."""
+    S = sum(h * w for h, w in LEVELS)
+    for geom in ("enc-init", "enc-spread2", "dec"):
+        v, sh, ls, loc, attn, go = inputs(900 if geom == "dec" else S, torch.bfloat16)
+        if geom == "enc-init":
+            loc = init_geometry_loc(2)
+        lq = loc.shape[1]
+        ref = None
+        for name, env in reversed(BWD_VARIANTS):
+            saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC")}
+            for k in saved:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            try:
+                fn = lambda: msda.ms_deform_attn_backward(v, sh, ls, loc, attn, go, 64,  # noqa: E731
+                                                          grad_value_dtype=torch.bfloat16, host_shapes=LEVELS)
+                out = fn()
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = [t.float().clone() for t in out]
+                err = [float((a.float() - b).abs().max() / b.abs().max()) for a, b in zip(out, ref)]
+                t = time_it(fn, iters)
+            finally:
+                for k, val in saved.items():
+                    os.environ.pop(k, None)
+                    if val is not None:
+                        os.environ[k] = val
+            sg = 2 if name.startswith("sorted") else 4
+            bb = msda.algorithmic_bytes("bwd", 2, S, 8, 32, 4, lq, 4, 2, sg=sg)
+            print(json.dumps(dict(geom=geom, variant=name, bwd_us=t * 1e6, algo_MB=bb / 1e6, bwd_GBps=bb / t / 1e9,
+                                  frac=bb / t / PEAK, rel_err_vs_lane32=err)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fwd-variants", action="store_true")
@@ -196,7 +240,11 @@ def main():
     ap.add_argument("--enc-variants", action="store_true")
     ap.add_argument("--enc-probes", action="store_true")
     ap.add_argument("--enc-caps", action="store_true")
+    ap.add_argument("--bwd-variants", action="store_true")
     args = ap.parse_args()
+    if args.bwd_variants:
+        bwd_variants(args.iters)
+        return
     if args.fwd_variants:
         fwd_variants(args.iters)
         return
