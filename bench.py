@@ -53,8 +53,10 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--forward-only", action="store_true",
                     help="BASELINE config 2: eval-mode forward (no autograd) instead of the train step")
-    ap.add_argument("--graphs", action="store_true",
-                    help="replay forward_core (fwd+bwd) as HIP graphs (experimental, 1 GPU; DESIGN.md §7)")
+    ap.add_argument("--graphs", dest="graphs", action="store_true", default=None,
+                    help="replay forward_core (fwd+bwd) as HIP graphs (default for the train step on the GPU; "
+                         "DESIGN.md section 7)")
+    ap.add_argument("--no-graphs", dest="graphs", action="store_false", help="eager train step")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
     ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
@@ -222,8 +224,8 @@ def pmc_traffic(kname, bs):
         return None
     kind, lq = kname
     with open(files[-1]) as f:
-        rows = [k for k in json.load(f)["kernels"]
-                if f"msda_{kind}" in k["kernel"] and k["traffic_bytes"] is not None]
+        allrows = json.load(f)["kernels"]
+    rows = [k for k in allrows if f"msda_{kind}" in k["kernel"] and k["traffic_bytes"] is not None]
     if not rows:
         return None
     # the launch grid is chosen inside the C-ABI (direct, lane32 or pixel-tiled
@@ -231,6 +233,17 @@ def pmc_traffic(kname, bs):
     # thousands of queries) has the largest grid of its kernel, the decoder
     # call (Lq = 900) the smallest
     pick = max if lq > 900 else min
+    if kind == "bwd" and any("msda_bwd_samples" in k["kernel"] for k in rows):
+        # the sorted backward is several kernels per call (per-sample pass,
+        # cell scan, scatter, [sort], per-destination sum): sum one row per
+        # kernel, each at the encoder's (largest) or decoder's grid
+        fam = [k for k in allrows if k["traffic_bytes"] is not None and
+               any(t in k["kernel"] for t in ("msda_bwd_samples", "msda_bwd_scatter", "msda_bwd_sort_cells",
+                                              "msda_bwd_value", "scan_block_sums", "scan_bsums", "scan_finish"))]
+        by = {}
+        for k in fam:
+            by.setdefault(k["kernel"], []).append(k)
+        return sum(pick(v, key=lambda k: k["grid"])["traffic_bytes"] for v in by.values())
     return pick(rows, key=lambda k: k["grid"])["traffic_bytes"]
 
 
@@ -267,12 +280,23 @@ def main(argv=None, device_type="cuda", child_script=None):
     args = make_args(device=str(device), backbone=a.backbone)
     model, criterion, _, optimizer = build_training(args, device)
     model.train(not a.forward_only)
+    # HIP graphs: the default for the train step on the
+    # GPU; the forward-only line and CPU contract runs stay eager
+    use_graphs = (a.graphs if a.graphs is not None else True) and on_gpu and not a.forward_only
+    core = model
+    grad_sync = None
     if world > 1 and not a.forward_only:
-        # reference main.py:258-261 (DDP + static graph); buckets sized for
-        # xGMI rings (fewer, larger all-reduces), launched as backward
-        # produces them so RCCL overlaps the rest of the backward pass
-        model = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local] if on_gpu else None, bucket_cap_mb=a.bucket_mb, static_graph=True)
+        if use_graphs:
+            # DDP's bucket hooks cannot fire inside a graph replay: the same
+            # averaged gradients by a bucketed RCCL all-reduce after backward
+            from gdino_amd.train import GradAllReduce
+            grad_sync = GradAllReduce(model.parameters(), a.bucket_mb)
+        else:
+            # reference main.py:258-261 (DDP + static graph); buckets sized for
+            # xGMI rings (fewer, larger all-reduces), launched as backward
+            # produces them so RCCL overlaps the rest of the backward pass
+            model = torch.nn.parallel.DistributedDataParallel(
+                model, device_ids=[local] if on_gpu else None, bucket_cap_mb=a.bucket_mb, static_graph=True)
     samples, targets, captions, cats = synthetic_batch(a.bs, a.height, a.width, n_boxes=8, n_tokens=256,
                                                        seed=1000 + rank, device=device)
     if a.forward_only:
@@ -281,24 +305,31 @@ def main(argv=None, device_type="cuda", child_script=None):
             return out["pred_logits"].float().nan_to_num(0.0, 0.0, 0.0).abs().mean()
     else:
         def step():
-            return train_step(model, criterion, optimizer, samples, targets, captions, cats)
+            return train_step(model, criterion, optimizer, samples, targets, captions, cats, grad_sync=grad_sync)
 
-    if a.graphs:
-        if world > 1 or a.forward_only:
-            raise SystemExit("--graphs is single-GPU train-step only")
-        print("warning: --graphs is experimental (DESIGN.md section 7)", file=sys.stderr, flush=True)
+    graph_note = None
+    if use_graphs:
         # GEMM library inside the captured region (GDINO_GRAPH_BLAS: "hipblaslt"
-        # or "cublas" = rocBLAS on ROCm; DESIGN.md section 7)
+        # or "cublas" = rocBLAS on ROCm)
         blas = os.environ.get("GDINO_GRAPH_BLAS")
         if blas:
             torch.backends.cuda.preferred_blas_library(blas)
-            print(f"graphs: preferred BLAS library {torch.backends.cuda.preferred_blas_library()}",
-                  file=sys.stderr, flush=True)
         from gdino_amd import graphs
-        text, _ = model.prepare_text(captions, device)
-        graphs.capture(model, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
-                               text["text_token_mask"], text["self_masks"], text["position_ids"]))
-        sync()
+        # MSDA launches inside the capture carry external timing events: the
+        # roofline below reads the last timed replay's launch times
+        msda.timer = msda.LaunchTimer()
+        try:
+            text, _ = core.prepare_text(captions, device)
+            graphs.capture(core, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
+                                  text["text_token_mask"], text["self_masks"], text["position_ids"]))
+            sync()
+        except Exception as e:  # capture refused: measure the eager step instead
+            graphs.release(core)
+            use_graphs = False
+            graph_note = f"graph capture failed, eager step measured: {repr(e)[:200]}"
+            print(f"warning: {graph_note}", file=sys.stderr, flush=True)
+        if not use_graphs:
+            msda.timer = None
 
     for _ in range(a.warmup):
         step()
@@ -306,7 +337,8 @@ def main(argv=None, device_type="cuda", child_script=None):
     if world > 1:
         dist.barrier()
 
-    msda.timer = msda.LaunchTimer()
+    if not use_graphs:
+        msda.timer = msda.LaunchTimer()
     sync()
     if world > 1:
         dist.barrier()
@@ -332,7 +364,7 @@ def main(argv=None, device_type="cuda", child_script=None):
     else:
         step_ms = [(b - a_) * 1e3 for a_, b in zip([t0] + host_marks[:-1], host_marks)]
     step_stats = _dist_stats(step_ms)
-    kern = msda.timer.summary()
+    kern = msda.timer.summary(captured=use_graphs) if msda.timer is not None else {}
     msda.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=device)
@@ -348,6 +380,9 @@ def main(argv=None, device_type="cuda", child_script=None):
     # also move the weights)
     hip_calls = None
     if on_gpu and world == 1:
+        if use_graphs:  # the extra step runs eagerly: every C-ABI call is a Python call
+            from gdino_amd import graphs
+            graphs.release(core)
         _lib.call_timer = _lib.CallTimer()
         try:
             step()
@@ -359,8 +394,8 @@ def main(argv=None, device_type="cuda", child_script=None):
 
     images = a.bs * world * a.steps
     value = images / elapsed
-    # dominant MSDA launch = largest total time (none recorded when the
-    # launches are inside HIP-graph replays: use the eager run's line)
+    # dominant MSDA launch = largest total time (graph mode: the launches of
+    # the last timed replay, via the capture's external timing events)
     roofline = None
     if kern:
         kname, kd = max(kern.items(), key=lambda kv: kv[1]["ms"])
@@ -369,7 +404,9 @@ def main(argv=None, device_type="cuda", child_script=None):
         roofline = {"bound": "hbm", "kernel": f"msda_{kname[0]} (Lq={kname[1]})",
                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK, "traffic": pmc_traffic(kname, a.bs),
-                    "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"]}
+                    "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"],
+                    "timed": ("HIP events inside the captured graph, last timed replay" if use_graphs else
+                              "HIP events on the launch stream over the timed region")}
     kernels = {f"msda_{k}_lq{lq}": {"launches": d["n"], "avg_us": d["ms"] / d["n"] * 1e3,
                                      "algo_bytes": d["bytes"], "GBps": d["bytes"] / (d["ms"] / d["n"] * 1e-3) / 1e9}
                for (k, lq), d in sorted(kern.items())}
@@ -400,11 +437,13 @@ def main(argv=None, device_type="cuda", child_script=None):
             "roofline": roofline,
             "kernels": kernels,
             "hip_entry_points_one_step": hip_calls,
-            "options": {"hip_graphs": bool(a.graphs), "tunableop": a.tunableop,
+            "options": {"hip_graphs": bool(use_graphs), "graph_note": graph_note, "tunableop": a.tunableop,
+                        "grad_sync": ("bucketed all-reduce after the graphed backward" if grad_sync is not None
+                                      else ("DDP" if world > 1 and not a.forward_only else None)),
                         # HIP kernel families on this run (GDINO_DISABLE turns them off for A/B)
                         "hip_families": ["msda", "biattn"] + [f for f in ("wattn", "attn", "contrastive", "prologue",
                                                                          "wgrad", "addln") if _lib.enabled(f)],
-                        "msda_bwd": os.environ.get("GD_MSDA_BWD", "auto")},
+                        "msda_bwd": os.environ.get("GD_MSDA_BWD", "sorted")},
             "loss": loss_v,
         }
         if not math.isfinite(loss_v):

@@ -361,7 +361,7 @@ namespace {
 struct SortedPlan {
   SortGeo G;
   int ncells = 0, nsamples = 0, nb = 0, k1_blocks = 0;
-  size_t o_cnt = 0, o_off = 0, o_bsum = 0, o_ids = 0, o_scr = 0, bytes = 0;
+  size_t o_cnt = 0, o_off = 0, o_bsum = 0, o_rank = 0, o_ids = 0, o_scr = 0, bytes = 0;
 };
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -391,37 +391,39 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
     return false;
   G.cpn = int(cpn);
   G.N = N;
-  // K4 splits: about 24-48 entries per lane group (a pixel is a corner of
-  // 4 cells; a level-l cell holds ~Lq * P / (H W) samples of each (n, m))
-  const int lpu = dt == GD_BF16 ? 4 : 8, gpb = 256 / lpu, maxF = 64 / lpu;
+  // K4 lane groups: G lanes (4..64) per destination, ~8 entries per lane (a
+  // pixel is a corner of 4 cells; a level-l cell holds ~Lq * P / (H W)
+  // samples of each (n, m))
+  const int lpu = dt == GD_BF16 ? 4 : 8, upb = 4 * (64 / lpu);  // K1 units per block
   int64_t bl = 0;
   for (int l = 0; l < 4; ++l) {
     const double e = 4.0 * double(Lq) * P / (double(G.H[l]) * G.W[l]);
-    int F = 1;
-    while (F < maxF && e / F > 48.0) F *= 2;
-    if (const char* ev = getenv("GD_MSDA_SORTED_F")) {  // A/B: fixed split for every level
+    int F = 4;
+    while (F < 64 && e / F > 8.0) F *= 2;
+    if (const char* ev = getenv("GD_MSDA_SORTED_F")) {  // A/B: fixed group size for every level
       const int f = atoi(ev);
-      if (f >= 1 && f <= maxF && (f & (f - 1)) == 0) F = f;
+      if (f >= 4 && f <= 64 && (f & (f - 1)) == 0) F = f;
     }
     G.F[l] = F;
     G.bstart[l] = int(bl);
-    bl += (int64_t(N) * G.H[l] * G.W[l] * M * F + gpb - 1) / gpb;
+    bl += (int64_t(N) * G.H[l] * G.W[l] * M * F + 255) / 256;
   }
+  if (int64_t(N) * M * S >= (int64_t(1) << 31)) return false;  // K4 item index
   if (bl >= (int64_t(1) << 31)) return false;
   G.bstart[4] = int(bl);
   pl.ncells = int(ncells);
   pl.nsamples = int(units * 16);
   pl.nb = int((ncells + kScanBlock - 1) / kScanBlock);
   if (pl.nb > 256 * kScanPer) return false;
-  const int upb = 4 * (64 / lpu);  // units per K1 block
   pl.k1_blocks = int((units + upb - 1) / upb);
   size_t o = 0;
-  pl.o_cnt = o; o = align_up(o + sizeof(int) * size_t(ncells));        // counts, then scatter cursor
+  pl.o_cnt = o; o = align_up(o + sizeof(int) * size_t(ncells));        // cell counts
   pl.o_off = o; o = align_up(o + sizeof(int) * size_t(ncells + 1));    // segment offsets
   pl.o_bsum = o; o = align_up(o + sizeof(int) * size_t(pl.nb));
-  pl.o_ids = o; o = align_up(o + sizeof(int) * size_t(pl.nsamples));   // sample ids by cell
+  pl.o_rank = o; o = align_up(o + sizeof(int) * size_t(pl.nsamples));  // rank of each sample in its cell
+  pl.o_ids = o; o = align_up(o + 16 * size_t(pl.nsamples));            // sample records by cell
   pl.o_scr = o;
-  if (flags & GD_MSDA_DETERMINISTIC) o = align_up(o + sizeof(int) * size_t(pl.nsamples));
+  if (flags & GD_MSDA_DETERMINISTIC) o = align_up(o + 16 * size_t(pl.nsamples));
   pl.bytes = o;
   return true;
 }
@@ -464,29 +466,35 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
   int* cnt = reinterpret_cast<int*>(w + pl.o_cnt);
   int* off = reinterpret_cast<int*>(w + pl.o_off);
   int* bsum = reinterpret_cast<int*>(w + pl.o_bsum);
-  int* ids = reinterpret_cast<int*>(w + pl.o_ids);
-  int* scr = reinterpret_cast<int*>(w + pl.o_scr);
+  int* rank = reinterpret_cast<int*>(w + pl.o_rank);
+  int4* ids = reinterpret_cast<int4*>(w + pl.o_ids);
+  int4* scr = reinterpret_cast<int4*>(w + pl.o_scr);
   const int units = pl.nsamples / 16;
   GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells), s));
   if (units > 0) {
-    if (dt == GD_BF16)
-      hipLaunchKernelGGL((msda_bwd_samples<uint16_t>), dim3(pl.k1_blocks), dim3(256), 0, s, (const uint16_t*)value,
-                         (const float*)loc, (const float*)attn, (const uint16_t*)grad_out, (float*)grad_loc,
-                         (float*)grad_attn, cnt, pl.G, S, Lq, M, units);
-    else
-      hipLaunchKernelGGL((msda_bwd_samples<float>), dim3(pl.k1_blocks), dim3(256), 0, s, (const float*)value,
-                         (const float*)loc, (const float*)attn, (const float*)grad_out, (float*)grad_loc,
-                         (float*)grad_attn, cnt, pl.G, S, Lq, M, units);
+    // K1 gathers one level at a time (default; fewer VGPRs: 169 vs 192 us at
+    // the encoder's init geometry, 379 vs 397 us on a 2-px spread) or with
+    // the next level in flight (GD_MSDA_SORTED_K1PIPE=1)
+    const bool pipe = env_int("GD_MSDA_SORTED_K1PIPE", 0) != 0;
+#define GD_K1(T, P)                                                                                              \
+  hipLaunchKernelGGL((msda_bwd_samples<T, P>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,             \
+                     (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_loc, (float*)grad_attn, \
+                     cnt, rank, pl.G, S, Lq, M, units)
+    if (dt == GD_BF16) {
+      if (pipe) GD_K1(uint16_t, true); else GD_K1(uint16_t, false);
+    } else {
+      if (pipe) GD_K1(float, true); else GD_K1(float, false);
+    }
+#undef GD_K1
     GD_LAUNCH_CHECK("msda_bwd_samples");
   }
   hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);
   hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(256), 0, s, bsum, pl.nb);
-  hipLaunchKernelGGL(scan_finish, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, (const int*)bsum, off,
-                     cnt);
+  hipLaunchKernelGGL(scan_finish, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, (const int*)bsum, off);
   GD_LAUNCH_CHECK("msda_bwd scan");
   if (units > 0) {
-    hipLaunchKernelGGL(msda_bwd_scatter, dim3((pl.nsamples + 255) / 256), dim3(256), 0, s, (const float*)loc, cnt,
-                       ids, pl.G, Lq, M, pl.nsamples);
+    hipLaunchKernelGGL(msda_bwd_scatter, dim3((pl.nsamples + 255) / 256), dim3(256), 0, s, (const float*)loc,
+                       (const float*)attn, (const int*)off, (const int*)rank, ids, pl.G, Lq, M, pl.nsamples);
     GD_LAUNCH_CHECK("msda_bwd_scatter");
     if (flags & GD_MSDA_DETERMINISTIC) {
       int bits = 1;
@@ -496,10 +504,10 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       GD_LAUNCH_CHECK("msda_bwd_sort_cells");
     }
   }
+  const int probe = env_int("GD_MSDA_SORTED_PROBE", 0);
 #define GD_K4(T, TO)                                                                                            \
   hipLaunchKernelGGL((msda_bwd_value<T, TO>), dim3(pl.G.bstart[4]), dim3(256), 0, s, (const T*)grad_out,        \
-                     (const float*)loc, (const float*)attn, (const int*)off, (const int*)ids, (TO*)grad_value, pl.G, \
-                     S, M)
+                     (const int*)off, (const int4*)ids, (TO*)grad_value, pl.G, S, M, probe)
   if (dt == GD_BF16 && gv_dt == GD_BF16) GD_K4(uint16_t, uint16_t);
   else if (dt == GD_BF16) GD_K4(uint16_t, float);
   else GD_K4(float, float);

@@ -111,7 +111,10 @@ def _token_linear_ok(x, params, out_features, dt):
     trainable fp32 parameters.  -> "splitk" (split-K weight-gradient kernel,
     a qualifying token-heavy shape), "lib" (library GEMM with fp32 output) or
     None (autocast's own path)."""
-    if dt != torch.bfloat16 or not torch.is_grad_enabled() or _capturing(params[0]):
+    # (also inside a HIP-graph capture: the split-K kernel and the fp32-output
+    # library GEMM are capturable; without them a captured backward ran the
+    # bf16 library GEMMs + a cast kernel per weight, +25 ms per step)
+    if dt != torch.bfloat16 or not torch.is_grad_enabled():
         return None
     if any(p.dtype != torch.float32 or not p.requires_grad for p in params):
         return None

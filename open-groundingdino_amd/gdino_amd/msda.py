@@ -53,26 +53,38 @@ def backward_variant() -> str:
 class LaunchTimer:
     """Optional HIP-event bracketing of every MSDA launch (bench.py's live
     roofline measurement).  Events are recorded on the launch stream (torch's
-    current stream, which is where the C-ABI call enqueues the kernel)."""
+    current stream, which is where the C-ABI call enqueues the kernel).
+
+    Inside a HIP-graph capture the events are created ``external``: they
+    become event-record nodes of the graph and are re-recorded by every
+    replay, so after a timed loop of replays they hold the LAST replay's
+    launch times (``summary(captured=True)``)."""
 
     def __init__(self):
-        self.records = []  # (kind, lq, bytes, start_event, end_event)
+        self.records = []  # (kind, lq, bytes, start_event, end_event, captured)
+
+    @staticmethod
+    def _event():
+        cap = torch.cuda.is_current_stream_capturing()
+        ev = torch.cuda.Event(enable_timing=True, external=cap)
+        ev.record()
+        return ev, cap
 
     def begin(self):
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        return ev
+        return self._event()
 
     def end(self, kind, lq, nbytes, start):
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        self.records.append((kind, lq, nbytes, start, ev))
+        ev, cap = self._event()
+        self.records.append((kind, lq, nbytes, start[0], ev, cap and start[1]))
 
-    def summary(self):
-        if self.records:
+    def summary(self, captured=False):
+        """{(kind, Lq): {"n", "ms", "bytes"}} over the eager launches, or
+        (captured=True) over the launches recorded inside a graph capture."""
+        recs = [r for r in self.records if r[5] == captured]
+        if recs:
             torch.cuda.synchronize()
         out = {}
-        for kind, lq, nbytes, s, e in self.records:
+        for kind, lq, nbytes, s, e, _ in recs:
             d = out.setdefault((kind, lq), {"n": 0, "ms": 0.0, "bytes": nbytes})
             d["n"] += 1
             d["ms"] += s.elapsed_time(e)

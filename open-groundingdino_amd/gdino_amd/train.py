@@ -161,9 +161,45 @@ def weighted_loss(loss_dict, weight_dict):
     return (torch.stack(vals) * w).sum()
 
 
+class GradAllReduce:
+    """Data-parallel gradient averaging after the backward pass, for the
+    HIP-graph train step (DDP's per-bucket hooks cannot fire inside a graph
+    replay): the gradients are all-reduced in buckets of ``bucket_mb``
+    (fewer, larger RCCL ring all-reduces over xGMI), then divided by the
+    world size -- DDP's result (reference main.py:258-261), without the
+    overlap with the backward.  Parameters without a gradient are skipped
+    (every rank runs the same graph, so the pattern agrees)."""
+
+    def __init__(self, params, bucket_mb: int = 64, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.params = [p for p in params if p.requires_grad]
+        self.bucket_bytes = bucket_mb << 20
+
+    def __call__(self):
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        world = self.dist.get_world_size(self.group)
+        grads = [p.grad for p in self.params if p.grad is not None]
+        bucket, size = [], 0
+        for g in grads + [None]:
+            if g is not None and (not bucket or (size + g.numel() * g.element_size() <= self.bucket_bytes
+                                                 and g.dtype == bucket[0].dtype)):
+                bucket.append(g)
+                size += g.numel() * g.element_size()
+                continue
+            if bucket:
+                flat = _flatten_dense_tensors(bucket)
+                self.dist.all_reduce(flat, group=self.group)
+                flat.div_(world)
+                torch._foreach_copy_(bucket, _unflatten_dense_tensors(flat, bucket))
+            bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
+
+
 def train_step(model, criterion, optimizer, samples, targets, captions, cat_lists, clip_max_norm=0.1,
-               amp_dtype=torch.bfloat16):
-    """One optimisation step; returns the weighted loss tensor (not synced)."""
+               amp_dtype=torch.bfloat16, grad_sync=None):
+    """One optimisation step; returns the weighted loss tensor (not synced).
+    ``grad_sync``: called between backward and clipping (GradAllReduce in
+    the multi-GPU HIP-graph step)."""
     dev_type = samples.tensors.device.type
     with torch.autocast(device_type=dev_type, dtype=amp_dtype, enabled=amp_dtype is not None):
         outputs = model(samples, captions=captions)
@@ -171,6 +207,8 @@ def train_step(model, criterion, optimizer, samples, targets, captions, cat_list
         loss = weighted_loss(loss_dict, criterion.weight_dict)
     optimizer.zero_grad(set_to_none=True)
     loss.backward()
+    if grad_sync is not None:
+        grad_sync()
     if clip_max_norm > 0:
         torch.nn.utils.clip_grad_norm_(model.parameters(), clip_max_norm, foreach=True)
     optimizer.step()

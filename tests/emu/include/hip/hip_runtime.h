@@ -55,6 +55,10 @@ struct dim3 {
 struct float2 { float x, y; };
 struct float4 { float x, y, z, w; };
 struct uint2 { unsigned x, y; };
+struct int2 { int x, y; };
+struct int4 { int x, y, z, w; };
+inline int2 make_int2(int a, int b) { return {a, b}; }
+inline int4 make_int4(int a, int b, int c, int d) { return {a, b, c, d}; }
 struct uint4 { unsigned x, y, z, w; };
 inline float2 make_float2(float a, float b) { return {a, b}; }
 inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
@@ -213,6 +217,13 @@ inline V shfl_xor(V v, int mask, int width) {
   return xchg_from(v, wave_base() + src);
 }
 
+template <typename V>
+inline V shfl(V v, int src, int width) {
+  const unsigned lane = lane_id();
+  const unsigned w = unsigned(width);
+  return xchg_from(v, wave_base() + ((lane & ~(w - 1)) | (unsigned(src) & (w - 1))));
+}
+
 // v_readlane: lane `src` of the caller's wave (a wave-uniform result)
 inline int readlane(int v, int src) { return xchg_from(v, wave_base() + unsigned(src)); }
 
@@ -341,8 +352,11 @@ void launch(dim3 g, dim3 b, F&& f) {
 #define __syncthreads() ::gd_emu::syncthreads()
 #define __ballot(pred) ::gd_emu::ballot(pred)
 #define __threadfence() ((void)0)  // one OS thread: memory is coherent
+#define __threadfence_block() ((void)0)
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 #define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
+#define __shfl(v, src, width) ::gd_emu::shfl((v), (src), (width))
 #define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
 // compiler scheduling hints: no semantics to emulate
 #define __builtin_amdgcn_sched_barrier(mask) ((void)(mask))

@@ -71,3 +71,57 @@ def test_ddp_two_ranks_gloo():
     assert p0 and p1, "parameters differ across ranks after the optimizer step"
     assert l0 != l1, "ranks should have seen different batches"
     assert s0 > 0
+
+
+def _worker_grad_allreduce(rank, world, port, q):
+    """GradAllReduce (the multi-GPU HIP-graph step's gradient averaging)
+    against DDP on the same model, batches and seeds: identical gradients
+    (DDP also averages over ranks) after one step, small buckets so the
+    bucket boundaries are exercised."""
+    sys.path[:0] = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "open-groundingdino_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle_hooks import oracle_msda
+        from gdino_amd.config import make_args
+        from gdino_amd.train import GradAllReduce, build_training, synthetic_batch, train_step
+        args = make_args(device="cpu", num_queries=50, enc_layers=2, dec_layers=2)
+        samples, targets, caps, cats = synthetic_batch(1, 96, 128, n_boxes=2, n_tokens=20, seed=200 + rank,
+                                                       device="cpu")
+        grads = {}
+        for mode in ("ddp", "manual"):
+            torch.manual_seed(0)
+            model, criterion, _, opt = build_training(args, "cpu")
+            for m in model.modules():  # the same function in both runs
+                if isinstance(m, torch.nn.Dropout):
+                    m.p = 0.0
+                if hasattr(m, "drop_prob"):
+                    m.drop_prob = 0.0
+            opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=0.0)
+            if mode == "ddp":
+                net, sync = torch.nn.parallel.DistributedDataParallel(model), None
+            else:
+                net, sync = model, GradAllReduce(model.parameters(), bucket_mb=1)
+            with oracle_msda():
+                train_step(net, criterion, opt, samples, targets, caps, cats, amp_dtype=None, clip_max_norm=0.0,
+                           grad_sync=sync)
+            grads[mode] = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None])
+        q.put((rank, float((grads["ddp"] - grads["manual"]).abs().max()), float(grads["ddp"].abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_matches_ddp_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_grad_allreduce, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs)
+    for _, diff, scale in res:
+        assert diff <= 1e-6 * max(scale, 1.0), res

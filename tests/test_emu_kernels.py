@@ -152,15 +152,15 @@ def test_emulated_sorted_backward_bf16_grad_value_and_determinism():
     assert E.rel_err(d1[0].double(), gv32.double().numpy()) < 1e-6
 
 
-def test_emulated_sorted_backward_long_cell_segments():
-    """Cells holding > 64 samples take the deterministic mode's wave radix
-    sort (not the register bitonic): every query samples the same few
-    points."""
+@pytest.mark.parametrize("lq", [90, 300])
+def test_emulated_sorted_backward_long_cell_segments(lq):
+    """Cells holding > 64 samples take the deterministic mode's LDS bitonic
+    sort (<= 1024: 90 queries x 4 points) or its wave radix sort (> 1024:
+    300 x 4): every query samples the same few points."""
     levels = [(3, 4), (2, 2), (1, 2), (1, 1)]
-    S = sum(h * w for h, w in levels)
-    value, shapes, lsi, loc, attn, grad_out = _levels_inputs(levels, 1, 90, seed=13)
+    value, shapes, lsi, loc, attn, grad_out = _levels_inputs(levels, 1, lq, seed=13)
     g = torch.Generator().manual_seed(3)
-    loc = (torch.rand(1, 90, 8, 4, 4, 2, generator=g) * 0.05 + 0.3)  # all in one cell per level
+    loc = (torch.rand(1, lq, 8, 4, 4, 2, generator=g) * 0.05 + 0.3)  # all in one cell per level
     _check_sorted((value, shapes, lsi, loc, attn, grad_out), levels, 1e-5, deterministic=True)
 
 

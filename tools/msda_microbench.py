@@ -191,6 +191,10 @@ def fwd_variants(iters):
 
 BWD_VARIANTS = [
     ("sorted", {"GD_MSDA_BWD": "sorted"}),
+    ("sorted probe no-g", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_PROBE": "1"}),
+    ("sorted probe no-recs", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_PROBE": "4"}),
+    ("sorted probe none", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_PROBE": "5"}),
+    ("sorted K1 single", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1PIPE": "0"}),
     ("sorted deterministic", {"GD_MSDA_BWD": "sorted", "GD_MSDA_DETERMINISTIC": "1"}),
     ("enc", {"GD_MSDA_BWD": "enc"}),
     ("lane32", {"GD_MSDA_BWD": "lane32"}),
@@ -209,7 +213,8 @@ def bwd_variants(iters):
         lq = loc.shape[1]
         ref = None
         for name, env in reversed(BWD_VARIANTS):
-            saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC")}
+            saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC", "GD_MSDA_SORTED_PROBE",
+                                                    "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
