@@ -315,9 +315,6 @@ def main(argv=None, device_type="cuda", child_script=None):
         if blas:
             torch.backends.cuda.preferred_blas_library(blas)
         from gdino_amd import graphs
-        # MSDA launches inside the capture carry external timing events: the
-        # roofline below reads the last timed replay's launch times
-        msda.timer = msda.LaunchTimer()
         try:
             text, _ = core.prepare_text(captions, device)
             graphs.capture(core, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
@@ -328,8 +325,6 @@ def main(argv=None, device_type="cuda", child_script=None):
             use_graphs = False
             graph_note = f"graph capture failed, eager step measured: {repr(e)[:200]}"
             print(f"warning: {graph_note}", file=sys.stderr, flush=True)
-        if not use_graphs:
-            msda.timer = None
 
     for _ in range(a.warmup):
         step()
@@ -337,8 +332,10 @@ def main(argv=None, device_type="cuda", child_script=None):
     if world > 1:
         dist.barrier()
 
-    if not use_graphs:
-        msda.timer = msda.LaunchTimer()
+    # MSDA launch timing over the timed region (eager); with graphs the
+    # launches are inside the replays, where ROCm refuses timing events: they
+    # are timed in the eager step that follows the timed region
+    msda.timer = None if use_graphs else msda.LaunchTimer()
     sync()
     if world > 1:
         dist.barrier()
@@ -364,7 +361,7 @@ def main(argv=None, device_type="cuda", child_script=None):
     else:
         step_ms = [(b - a_) * 1e3 for a_, b in zip([t0] + host_marks[:-1], host_marks)]
     step_stats = _dist_stats(step_ms)
-    kern = msda.timer.summary(captured=use_graphs) if msda.timer is not None else {}
+    kern = msda.timer.summary() if msda.timer is not None else {}
     msda.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=device)
@@ -383,14 +380,18 @@ def main(argv=None, device_type="cuda", child_script=None):
         if use_graphs:  # the extra step runs eagerly: every C-ABI call is a Python call
             from gdino_amd import graphs
             graphs.release(core)
+            msda.timer = msda.LaunchTimer()
         _lib.call_timer = _lib.CallTimer()
         try:
             step()
             hip_calls = _lib.call_timer.summary()
+            if use_graphs:
+                kern = msda.timer.summary()
         except Exception as e:  # diagnostics only: never cost the bench line
             hip_calls = {"error": repr(e)[:300]}
         finally:
             _lib.call_timer = None
+            msda.timer = None
 
     images = a.bs * world * a.steps
     value = images / elapsed
@@ -405,7 +406,8 @@ def main(argv=None, device_type="cuda", child_script=None):
                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK, "traffic": pmc_traffic(kname, a.bs),
                     "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"],
-                    "timed": ("HIP events inside the captured graph, last timed replay" if use_graphs else
+                    "timed": ("HIP events on the launch stream in one eager step right after the timed graph "
+                              "replays (ROCm refuses timing events inside a graph capture)" if use_graphs else
                               "HIP events on the launch stream over the timed region")}
     kernels = {f"msda_{k}_lq{lq}": {"launches": d["n"], "avg_us": d["ms"] / d["n"] * 1e3,
                                      "algo_bytes": d["bytes"], "GBps": d["bytes"] / (d["ms"] / d["n"] * 1e-3) / 1e9}

@@ -361,7 +361,7 @@ namespace {
 struct SortedPlan {
   SortGeo G;
   int ncells = 0, nsamples = 0, nb = 0, k1_blocks = 0;
-  size_t o_cnt = 0, o_off = 0, o_bsum = 0, o_rank = 0, o_ids = 0, o_scr = 0, bytes = 0;
+  size_t o_cnt = 0, o_off = 0, o_bsum = 0, o_rank = 0, o_ids = 0, o_part = 0, o_scr = 0, bytes = 0;
 };
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -391,26 +391,26 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
     return false;
   G.cpn = int(cpn);
   G.N = N;
-  // K4 lane groups: G lanes (4..64) per destination, ~8 entries per lane (a
-  // pixel is a corner of 4 cells; a level-l cell holds ~Lq * P / (H W)
-  // samples of each (n, m))
+  // K4a splits: ~16 samples per lane group (a level-l cell holds about
+  // Lq * P / (H W) samples of each (n, m))
   const int lpu = dt == GD_BF16 ? 4 : 8, upb = 4 * (64 / lpu);  // K1 units per block
+  const int gpb = 256 / lpu, maxF = 64 / lpu;
   int64_t bl = 0;
   for (int l = 0; l < 4; ++l) {
-    const double e = 4.0 * double(Lq) * P / (double(G.H[l]) * G.W[l]);
-    int F = 4;
-    while (F < 64 && e / F > 8.0) F *= 2;
-    if (const char* ev = getenv("GD_MSDA_SORTED_F")) {  // A/B: fixed group size for every level
+    const double e = double(Lq) * P / (double(G.H[l]) * G.W[l]);
+    int F = 1;
+    while (F < maxF && e / F > 16.0) F *= 2;
+    if (const char* ev = getenv("GD_MSDA_SORTED_F")) {  // A/B: fixed split for every level
       const int f = atoi(ev);
-      if (f >= 4 && f <= 64 && (f & (f - 1)) == 0) F = f;
+      if (f >= 1 && f <= maxF && (f & (f - 1)) == 0) F = f;
     }
     G.F[l] = F;
-    G.bstart[l] = int(bl);
-    bl += (int64_t(N) * G.H[l] * G.W[l] * M * F + 255) / 256;
+    G.cstart[l] = int(bl);
+    bl += (int64_t(N) * M * (G.H[l] + 1) * (G.W[l] + 1) * F + gpb - 1) / gpb;
   }
-  if (int64_t(N) * M * S >= (int64_t(1) << 31)) return false;  // K4 item index
   if (bl >= (int64_t(1) << 31)) return false;
-  G.bstart[4] = int(bl);
+  G.cstart[4] = int(bl);
+  if (int64_t(N) * M * S >= (int64_t(1) << 31)) return false;  // K4 item index
   pl.ncells = int(ncells);
   pl.nsamples = int(units * 16);
   pl.nb = int((ncells + kScanBlock - 1) / kScanBlock);
@@ -422,6 +422,7 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
   pl.o_bsum = o; o = align_up(o + sizeof(int) * size_t(pl.nb));
   pl.o_rank = o; o = align_up(o + sizeof(int) * size_t(pl.nsamples));  // rank of each sample in its cell
   pl.o_ids = o; o = align_up(o + 16 * size_t(pl.nsamples));            // sample records by cell
+  pl.o_part = o; o = align_up(o + sizeof(float) * 128 * size_t(ncells));  // 4 corner partial rows per cell
   pl.o_scr = o;
   if (flags & GD_MSDA_DETERMINISTIC) o = align_up(o + 16 * size_t(pl.nsamples));
   pl.bytes = o;
@@ -469,6 +470,7 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
   int* rank = reinterpret_cast<int*>(w + pl.o_rank);
   int4* ids = reinterpret_cast<int4*>(w + pl.o_ids);
   int4* scr = reinterpret_cast<int4*>(w + pl.o_scr);
+  float* part = reinterpret_cast<float*>(w + pl.o_part);
   const int units = pl.nsamples / 16;
   GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells), s));
   if (units > 0) {
@@ -504,14 +506,23 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       GD_LAUNCH_CHECK("msda_bwd_sort_cells");
     }
   }
-  const int probe = env_int("GD_MSDA_SORTED_PROBE", 0);
-#define GD_K4(T, TO)                                                                                            \
-  hipLaunchKernelGGL((msda_bwd_value<T, TO>), dim3(pl.G.bstart[4]), dim3(256), 0, s, (const T*)grad_out,        \
-                     (const int*)off, (const int4*)ids, (TO*)grad_value, pl.G, S, M, probe)
-  if (dt == GD_BF16 && gv_dt == GD_BF16) GD_K4(uint16_t, uint16_t);
-  else if (dt == GD_BF16) GD_K4(uint16_t, float);
-  else GD_K4(float, float);
-#undef GD_K4
-  GD_LAUNCH_CHECK("msda_bwd_value");
+  if (dt == GD_BF16)
+    hipLaunchKernelGGL((msda_bwd_cellsum<uint16_t>), dim3(pl.G.cstart[4]), dim3(256), 0, s,
+                       (const uint16_t*)grad_out, (const int*)off, (const int4*)ids, part, pl.G, M);
+  else
+    hipLaunchKernelGGL((msda_bwd_cellsum<float>), dim3(pl.G.cstart[4]), dim3(256), 0, s, (const float*)grad_out,
+                       (const int*)off, (const int4*)ids, part, pl.G, M);
+  GD_LAUNCH_CHECK("msda_bwd_cellsum");
+  const int items = N * M * S;
+  const int lpu = dt == GD_BF16 ? 4 : 8;
+  const int pblocks = (items + 256 / lpu - 1) / (256 / lpu);
+#define GD_K4B(T, TO)                                                                                        \
+  hipLaunchKernelGGL((msda_bwd_pixsum<T, TO>), dim3(pblocks), dim3(256), 0, s, (const int*)off,              \
+                     (const float*)part, (TO*)grad_value, pl.G, S, M, items)
+  if (dt == GD_BF16 && gv_dt == GD_BF16) GD_K4B(uint16_t, uint16_t);
+  else if (dt == GD_BF16) GD_K4B(uint16_t, float);
+  else GD_K4B(float, float);
+#undef GD_K4B
+  GD_LAUNCH_CHECK("msda_bwd_pixsum");
   return GD_OK;
 }

@@ -45,46 +45,42 @@ def deterministic() -> bool:
 
 
 def backward_variant() -> str:
-    """GD_MSDA_BWD: sorted (default: atomic-free, csrc/msda_sorted.inc), or
-    the round-1/2 kernels for A/B runs: enc / lane32 / tiled."""
+    """GD_MSDA_BWD: sorted (default: the atomic-free csrc/msda_sorted.inc for
+    the encoder shape, lane32 for the decoder), sorted-all (sorted for every
+    call), or the round-1/2 kernels for A/B runs: enc / lane32 / tiled."""
     return os.environ.get("GD_MSDA_BWD", "sorted")
 
 
 class LaunchTimer:
     """Optional HIP-event bracketing of every MSDA launch (bench.py's live
     roofline measurement).  Events are recorded on the launch stream (torch's
-    current stream, which is where the C-ABI call enqueues the kernel).
-
-    Inside a HIP-graph capture the events are created ``external``: they
-    become event-record nodes of the graph and are re-recorded by every
-    replay, so after a timed loop of replays they hold the LAST replay's
-    launch times (``summary(captured=True)``)."""
+    current stream, which is where the C-ABI call enqueues the kernel).  Not
+    inside a HIP-graph capture: ROCm refuses timing events there (torch's
+    ``external`` events are disallowed), so launches replayed from a graph are
+    timed in an eager step instead (bench.py)."""
 
     def __init__(self):
-        self.records = []  # (kind, lq, bytes, start_event, end_event, captured)
-
-    @staticmethod
-    def _event():
-        cap = torch.cuda.is_current_stream_capturing()
-        ev = torch.cuda.Event(enable_timing=True, external=cap)
-        ev.record()
-        return ev, cap
+        self.records = []  # (kind, lq, bytes, start_event, end_event)
 
     def begin(self):
-        return self._event()
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
 
     def end(self, kind, lq, nbytes, start):
-        ev, cap = self._event()
-        self.records.append((kind, lq, nbytes, start[0], ev, cap and start[1]))
+        if start is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.records.append((kind, lq, nbytes, start, ev))
 
-    def summary(self, captured=False):
-        """{(kind, Lq): {"n", "ms", "bytes"}} over the eager launches, or
-        (captured=True) over the launches recorded inside a graph capture."""
-        recs = [r for r in self.records if r[5] == captured]
-        if recs:
+    def summary(self):
+        if self.records:
             torch.cuda.synchronize()
         out = {}
-        for kind, lq, nbytes, s, e, _ in recs:
+        for kind, lq, nbytes, s, e in self.records:
             d = out.setdefault((kind, lq), {"n": 0, "ms": 0.0, "bytes": nbytes})
             d["n"] += 1
             d["ms"] += s.elapsed_time(e)
@@ -196,7 +192,13 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     hs = None
     if host_shapes is not None and len(host_shapes) == L:
         hs = (ctypes.c_int64 * (2 * L))(*[int(v) for hw in host_shapes for v in hw])
-    if value.is_cuda and hs is not None and backward_variant() in ("sorted", "auto"):
+    variant = backward_variant()
+    # sorted: the encoder shape (Lq == S) by default; the decoder's 900
+    # score-sorted queries crowd a few cells (the lane-group walk then has a
+    # long tail: 173 us in the train step vs 114 us for the direct-atomic
+    # kernel), so it keeps msda_bwd_lane32 unless determinism is asked for
+    if value.is_cuda and hs is not None and (variant == "sorted" and (Lq == S or deterministic())
+                                             or variant == "sorted-all"):
         out = _backward_sorted(value, spatial_shapes, level_start_index, loc, attn, grad_output,
                                (N, S, M, D, L, Lq, P), hs, grad_value_dtype)
         if out is not None:

@@ -352,8 +352,9 @@ def test_encoder_enc_matches_direct_atomic_kernel(vdtype, monkeypatch):
 def test_sorted_backward_decoder_shape_800x1333(lq, vdtype, tol, monkeypatch):
     """The decoder's cross-attention (900 queries sampling anywhere, also
     outside the levels) through the sorted backward (host shapes given, as the
-    model passes them)."""
-    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    model passes them; GD_MSDA_BWD=sorted-all: by default the decoder shape
+    keeps the direct-atomic kernel)."""
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted-all")
     value, shapes, lsi, loc, attn, grad_out = _big_inputs(lq, seed=lq + 1, vdtype=vdtype)
     inputs = (value.cpu(), shapes, lsi, loc.cpu(), attn.cpu(), grad_out.cpu())
     _check_bwd_vs_oracle(inputs, tol, host_shapes=LEVELS_800)
@@ -380,7 +381,7 @@ def test_sorted_backward_deterministic_mode_is_bitwise_reproducible(lq, monkeypa
     so two runs give bitwise-equal grad_value (and grad_loc / grad_attn, which
     never use atomics).  bf16 value, grad_value written in bf16 as autograd
     takes it."""
-    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted-all")
     monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "1")
     if lq == 900:
         inputs = [t.to(DEV) for t in _big_inputs(900, seed=5, vdtype=torch.bfloat16)]

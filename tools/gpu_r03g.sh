@@ -2,7 +2,7 @@ set -o pipefail
 mkdir -p gpurun_out/g_prof
 export TMPDIR=/tmp
 T() { timeout -k 10 "$@"; }
-T 600 python3 -u -m pytest tests/test_msda_gpu.py -x -q --timeout 120 --timeout-method thread -k "sorted or pixel_block or init_geometry" > gpurun_out/g_msda_tests.log 2>&1
+T 600 python3 -u -m pytest tests/test_msda_gpu.py -x -q --timeout 120 --timeout-method thread -k "sorted or pixel_block or init_geometry or gradcheck or golden" > gpurun_out/g_msda_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/g_msda_tests.log
 [ $rc -ne 0 ] && exit $rc

@@ -191,10 +191,9 @@ def fwd_variants(iters):
 
 BWD_VARIANTS = [
     ("sorted", {"GD_MSDA_BWD": "sorted"}),
-    ("sorted probe no-g", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_PROBE": "1"}),
-    ("sorted probe no-recs", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_PROBE": "4"}),
-    ("sorted probe none", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_PROBE": "5"}),
-    ("sorted K1 single", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1PIPE": "0"}),
+    ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
+    ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
+    ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
     ("sorted deterministic", {"GD_MSDA_BWD": "sorted", "GD_MSDA_DETERMINISTIC": "1"}),
     ("enc", {"GD_MSDA_BWD": "enc"}),
     ("lane32", {"GD_MSDA_BWD": "lane32"}),
