@@ -59,6 +59,9 @@ def parse(argv=None):
     ap.add_argument("--no-graphs", dest="graphs", action="store_false", help="eager train step")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
+    ap.add_argument("--output-dir", default=None,
+                    help="reference main.py:347-434: resume from DIR/checkpoint.pth when present, save it after "
+                         "the timed steps (rank 0); outside the timed region")
     ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
                     help=argparse.SUPPRESS)  # cpu: the CPU contract tests only (HIP ops routed by the test)
     return ap.parse_args(argv)
@@ -280,6 +283,14 @@ def main(argv=None, device_type="cuda", child_script=None):
     args = make_args(device=str(device), backbone=a.backbone)
     model, criterion, _, optimizer = build_training(args, device)
     model.train(not a.forward_only)
+    start_epoch = 0
+    # reference main.py:339 (the cfg_odvg default: StepLR every lr_drop epochs)
+    sched = torch.optim.lr_scheduler.StepLR(optimizer, args.lr_drop)
+    if a.output_dir and not a.forward_only:
+        from gdino_amd import checkpoint as ckpt
+        path = ckpt.resume_path(a.output_dir)
+        if path is not None:
+            start_epoch = ckpt.resume(path, model, optimizer, sched)
     # HIP graphs: the default for the train step on the
     # GPU; the forward-only line and CPU contract runs stay eager
     use_graphs = (a.graphs if a.graphs is not None else True) and on_gpu and not a.forward_only
@@ -412,6 +423,11 @@ def main(argv=None, device_type="cuda", child_script=None):
     kernels = {f"msda_{k}_lq{lq}": {"launches": d["n"], "avg_us": d["ms"] / d["n"] * 1e3,
                                      "algo_bytes": d["bytes"], "GBps": d["bytes"] / (d["ms"] / d["n"] * 1e-3) / 1e9}
                for (k, lq), d in sorted(kern.items())}
+
+    if a.output_dir and not a.forward_only:
+        from gdino_amd import checkpoint as ckpt
+        ckpt.save_checkpoint(os.path.join(a.output_dir, "checkpoint.pth"), core, optimizer, sched, start_epoch,
+                             args)
 
     if rank == 0:
         mode = "forward (eval, no autograd)" if a.forward_only else "train step (fwd+bwd+AdamW)"

@@ -46,7 +46,12 @@ def _is_main() -> bool:
 
 def load_checkpoint(path: str, map_location="cpu") -> dict:
     """torch.load without executing anything from the file (weights_only),
-    accepting the argparse.Namespace the reference stores under 'args'."""
+    accepting the argparse.Namespace the reference stores under 'args'.
+    The reference's ``https`` branch (main.py:351-353, load_state_dict_from_url)
+    is rejected explicitly: there is no egress on the training hosts, and a
+    silent local-path fallback would hide a misconfigured --resume."""
+    if str(path).startswith(("http://", "https://")):
+        raise ValueError(f"resume from a URL is not supported (no network): {path}; download it and pass the path")
     with torch.serialization.safe_globals([argparse.Namespace]):
         return torch.load(path, map_location=map_location, weights_only=True)
 

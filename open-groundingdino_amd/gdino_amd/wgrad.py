@@ -84,7 +84,10 @@ def lib_eligible(x: torch.Tensor, dtype) -> bool:
     """Route a (non split-K) Linear's weight gradient to weight_grad_lib."""
     # a library GEMM (aten::mm.dtype exists for the ROCm device only): x.is_cuda,
     # not _lib.on_device, which the host-side emulator tests redirect
-    return FP32_OUT_GEMM and dtype == torch.bfloat16 and x.is_cuda
+    # honours the same kill switches as the split-K route (ENABLED,
+    # GDINO_DISABLE=wgrad), so the documented A/B off-switch covers both
+    return (ENABLED and _lib.enabled("wgrad") and FP32_OUT_GEMM and dtype == torch.bfloat16
+            and x.is_cuda)
 
 
 _MM_DTYPE_OK = True

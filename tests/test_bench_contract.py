@@ -133,3 +133,25 @@ def test_pmc_traffic_matches_the_encoder_and_decoder_launch_by_grid(tmp_path, mo
     assert bench.pmc_traffic(("fwd", 900), 2) == 1.6e8  # only the measured row
     (prof / "r01_pmc_traffic.json").write_text(json.dumps({"kernels": rows[2:3]}))
     assert bench.pmc_traffic(("bwd", 22223), 2) is None
+
+
+def test_bench_output_dir_resumes_and_saves(tmp_path, capsys):
+    """--output-dir (reference main.py:347-362, 414-434): the first run saves
+    DIR/checkpoint.pth after its timed steps; the second run resumes model,
+    optimizer and scheduler state from it and saves the next epoch."""
+    import bench
+    from gdino_amd.checkpoint import load_checkpoint
+    argv = ["--steps", "1", "--warmup", "0", "--height", "256", "--width", "320", "--no-cpu-baseline",
+            "--output-dir", str(tmp_path)]
+    torch.manual_seed(0)
+    with oracle_msda():
+        bench.main(argv, device_type="cpu")
+        ck0 = load_checkpoint(str(tmp_path / "checkpoint.pth"))
+        assert ck0["epoch"] == 0 and {"model", "optimizer", "lr_scheduler", "args"} <= set(ck0)
+        bench.main(argv, device_type="cpu")
+    ck1 = load_checkpoint(str(tmp_path / "checkpoint.pth"))
+    assert ck1["epoch"] == 1
+    # the optimizer state continued from the first run: AdamW's step counter is 2
+    steps = {int(v["step"]) for v in ck1["optimizer"]["state"].values()}
+    assert steps == {2}, steps
+    capsys.readouterr()
