@@ -237,12 +237,13 @@ def pmc_traffic(kname, bs):
     # call (Lq = 900) the smallest
     pick = max if lq > 900 else min
     if kind == "bwd" and any("msda_bwd_samples" in k["kernel"] for k in rows):
-        # the sorted backward is several kernels per call (per-sample pass,
-        # cell scan, scatter, [sort], per-destination sum): sum one row per
-        # kernel, each at the encoder's (largest) or decoder's grid
+        # the sorted backward is several kernels per call (cell count, scan,
+        # per-sample pass, [sort], per-cell and per-pixel sums): sum one row
+        # per kernel, each at the encoder's (largest) or decoder's grid
+        single = ("msda_bwd_lane32", "msda_bwd_enc", "msda_bwd_generic", "msda_bwd_tiled")
         fam = [k for k in allrows if k["traffic_bytes"] is not None and
-               any(t in k["kernel"] for t in ("msda_bwd_samples", "msda_bwd_scatter", "msda_bwd_sort_cells",
-                                              "msda_bwd_value", "scan_block_sums", "scan_bsums", "scan_finish"))]
+               (("msda_bwd_" in k["kernel"] and not any(t in k["kernel"] for t in single)) or
+                any(t in k["kernel"] for t in ("scan_block_sums", "scan_bsums", "scan_finish")))]
         by = {}
         for k in fam:
             by.setdefault(k["kernel"], []).append(k)

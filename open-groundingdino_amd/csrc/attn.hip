@@ -68,6 +68,22 @@ gd_status take_strides(int64_t dst[3], const int64_t* src, const void* p, gd_dty
   return GD_OK;
 }
 
+// Query tiles of 16 per wave: 4 (64-query waves, the K / V fragments of a
+// key block amortised over the most queries) unless that leaves fewer than
+// 1024 waves (4 per CU) -- BERT (24 (b, h) x 256 queries: 96 waves), the text
+// enhancer (32) and the decoder (240) -- then 1.  GD_ATTN_QT=1|4 forces it.
+int query_tiles(int Lq, int bh) {
+  const int f = env_int("GD_ATTN_QT", 0);
+  if (f == 1 || f == 4) return f;
+  return int64_t((Lq + 63) / 64) * bh >= 1024 ? 4 : 1;
+}
+// Key tiles of 16 per wave in the dK / dV kernel: 2, or 1 below 1024 waves.
+int key_tiles(int Lk, int bh) {
+  const int f = env_int("GD_ATTN_KT", 0);
+  if (f == 1 || f == 2) return f;
+  return int64_t((Lk + 31) / 32) * bh >= 1024 ? 2 : 1;
+}
+
 }  // namespace
 }  // namespace gd
 
@@ -93,19 +109,26 @@ extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, 
   a.o = out;
   a.lse = lse;
   hipStream_t s = as_hip(stream);
-  const dim3 grid(unsigned((Lq + 255) / 256), unsigned(B * H));
-#define GD_AF(T, HD)                                                                         \
+  const int qt = query_tiles(Lq, B * H);
+  const dim3 grid(unsigned((Lq + 64 * qt - 1) / (64 * qt)), unsigned(B * H));
+#define GD_AF1(T, HD, QT)                                                                    \
   do {                                                                                       \
     if (a.dropout)                                                                           \
-      hipLaunchKernelGGL((attn_fwd_kernel<T, HD, true>), grid, dim3(256), 0, s, a);          \
+      hipLaunchKernelGGL((attn_fwd_kernel<T, HD, true, QT>), grid, dim3(256), 0, s, a);      \
     else                                                                                     \
-      hipLaunchKernelGGL((attn_fwd_kernel<T, HD, false>), grid, dim3(256), 0, s, a);         \
+      hipLaunchKernelGGL((attn_fwd_kernel<T, HD, false, QT>), grid, dim3(256), 0, s, a);     \
+  } while (0)
+#define GD_AF(T, HD)                       \
+  do {                                     \
+    if (qt == 4) GD_AF1(T, HD, 4);         \
+    else GD_AF1(T, HD, 1);                 \
   } while (0)
   if (dt == GD_BF16) {
     if (head_dim == 32) GD_AF(uint16_t, 32); else GD_AF(uint16_t, 64);
   } else {
     if (head_dim == 32) GD_AF(float, 32); else GD_AF(float, 64);
   }
+#undef GD_AF1
 #undef GD_AF
   GD_LAUNCH_CHECK("attn_fwd");
   return GD_OK;
@@ -139,26 +162,29 @@ extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk,
   a.lse = const_cast<float*>(lse);
   a.dsum = dsum;
   hipStream_t s = as_hip(stream);
-  const dim3 gq(unsigned((Lq + 255) / 256), unsigned(B * H));
-  const dim3 gk(unsigned((Lk + 127) / 128), unsigned(B * H));
-#define GD_AB(T, HD)                                                                  \
-  do {                                                                                \
-    if (a.dropout) {                                                                  \
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD, true>), gq, dim3(256), 0, s, a);  \
-      GD_LAUNCH_CHECK("attn_bwd_dq");                                                 \
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD, true>), gk, dim3(256), 0, s, a); \
-    } else {                                                                          \
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD, false>), gq, dim3(256), 0, s, a); \
-      GD_LAUNCH_CHECK("attn_bwd_dq");                                                 \
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD, false>), gk, dim3(256), 0, s, a);\
-    }                                                                                 \
-    GD_LAUNCH_CHECK("attn_bwd_dkv");                                                  \
+  const int qt = query_tiles(Lq, B * H), kt = key_tiles(Lk, B * H);
+  const dim3 gq(unsigned((Lq + 64 * qt - 1) / (64 * qt)), unsigned(B * H));
+  const dim3 gk(unsigned((Lk + 64 * kt - 1) / (64 * kt)), unsigned(B * H));
+#define GD_AB1(T, HD, DR)                                                                                  \
+  do {                                                                                                     \
+    if (qt == 4) hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD, DR, 4>), gq, dim3(256), 0, s, a);           \
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<T, HD, DR, 1>), gq, dim3(256), 0, s, a);                   \
+    GD_LAUNCH_CHECK("attn_bwd_dq");                                                                        \
+    if (kt == 2) hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD, DR, 2>), gk, dim3(256), 0, s, a);          \
+    else hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, HD, DR, 1>), gk, dim3(256), 0, s, a);                  \
+    GD_LAUNCH_CHECK("attn_bwd_dkv");                                                                       \
+  } while (0)
+#define GD_AB(T, HD)                       \
+  do {                                     \
+    if (a.dropout) GD_AB1(T, HD, true);    \
+    else GD_AB1(T, HD, false);             \
   } while (0)
   if (dt == GD_BF16) {
     if (head_dim == 32) GD_AB(uint16_t, 32); else GD_AB(uint16_t, 64);
   } else {
     if (head_dim == 32) GD_AB(float, 32); else GD_AB(float, 64);
   }
+#undef GD_AB1
 #undef GD_AB
   return GD_OK;
 }

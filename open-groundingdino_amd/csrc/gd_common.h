@@ -6,6 +6,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
 #include "../../include/gdino_amd.h"
 
@@ -79,3 +80,10 @@ __device__ __forceinline__ float dpp(float v) {
 }
 
 }  // namespace gd
+
+// integer tuning / A-B switch from the environment (host side)
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+

@@ -35,6 +35,9 @@
 // this keeps the gathered rows in one XCD's L2).
 #include "gd_common.h"
 
+#include <algorithm>
+#include <cmath>
+
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -91,11 +94,6 @@ inline void enc_geometry(int (&th)[4], int (&tw)[4], int (&cap)[4]) {
       for (int l = 0; l < 4; ++l)
         if (v[l] >= 0) cap[l] = v[l];
   }
-}
-
-inline int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
 }
 
 inline int grid_for(int64_t total, int block) {
@@ -229,7 +227,10 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
     }
     tl.tstart[4] = int(nt);
     const int64_t blocks = int64_t(N) * nt * M;
-    if (ok && cover == S && blocks < (int64_t(1) << 31) && rows <= 1024) {
+    // the kernel's 32-bit byte offsets into value (msda_enc.inc) need
+    // N*S*M*D*sizeof(T) < 2^32, as the forward checks
+    const size_t vbytes = size_t(N) * S * M * D * (dt == GD_BF16 ? 2 : 4);
+    if (ok && cover == S && blocks < (int64_t(1) << 31) && rows <= 1024 && vbytes < (size_t(1) << 32)) {
       const int rmax = env_int("GD_MSDA_ENC_RMAX", 8);
       const int mode = env_int("GD_MSDA_ENC_MODE", 0);  // 1: ds_add_f32 instead of read-modify-write
       // gathers of 1 unit in flight (default, measured 0.84 ms) or 2
@@ -360,8 +361,10 @@ namespace {
 
 struct SortedPlan {
   SortGeo G;
+  SweepGeo W;
   int ncells = 0, nsamples = 0, nb = 0, k1_blocks = 0;
-  size_t o_cnt = 0, o_off = 0, o_bsum = 0, o_rank = 0, o_ids = 0, o_part = 0, o_scr = 0, bytes = 0;
+  size_t o_sweep = 0;  // K4 sweep: partial rows of the chunked levels
+  size_t o_cnt = 0, o_off = 0, o_cur = 0, o_bsum = 0, o_ids = 0, o_part = 0, o_scr = 0, bytes = 0;
 };
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -420,9 +423,44 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
   pl.o_cnt = o; o = align_up(o + sizeof(int) * size_t(ncells));        // cell counts
   pl.o_off = o; o = align_up(o + sizeof(int) * size_t(ncells + 1));    // segment offsets
   pl.o_bsum = o; o = align_up(o + sizeof(int) * size_t(pl.nb));
-  pl.o_rank = o; o = align_up(o + sizeof(int) * size_t(pl.nsamples));  // rank of each sample in its cell
+  pl.o_cur = o; o = align_up(o + sizeof(int) * size_t(ncells));        // segment cursors (K1)
   pl.o_ids = o; o = align_up(o + 16 * size_t(pl.nsamples));            // sample records by cell
-  pl.o_part = o; o = align_up(o + sizeof(float) * 128 * size_t(ncells));  // 4 corner partial rows per cell
+  // K4 sweep geometry (msda_sorted.inc): a wave = GPW - 1 pixel columns x R
+  // rows of one (n, m, level) [x Gs record chunks].  lam = samples per cell
+  // of one (n, m) on level l; chunks keep <= 32 records per cell and wave,
+  // rows ~128 records per lane group and task.
+  {
+    SweepGeo& W = pl.W;
+    const int gpw = 64 / lpu;
+    int64_t tasks = 0, items = 0, pfl = 0;
+    for (int l = 0; l < 4; ++l) {
+      const int H = G.H[l], Wd = G.W[l];
+      const double lam = double(Lq) * P / (double(H) * Wd);
+      int Gs = 1;
+      while (Gs < 64 && lam / Gs > 32.0) Gs *= 2;
+      const double per = std::max(lam / Gs, 1.0);
+      const int R = int(std::min<double>(H, std::max(2.0, std::floor(128.0 / per))));
+      W.Gs[l] = Gs;
+      W.R[l] = R;
+      W.bands[l] = (Wd + gpw - 2) / (gpw - 1);
+      W.rblk[l] = (H + R - 1) / R;
+      W.tstart[l] = int(tasks);
+      tasks += int64_t(N) * M * W.bands[l] * W.rblk[l] * Gs;
+      W.cstart[l] = int(items);
+      W.pbase[l] = pfl;
+      if (Gs > 1) {
+        items += int64_t(N) * M * H * Wd;
+        pfl += int64_t(N) * M * H * Wd * Gs * D;
+      }
+    }
+    W.tstart[4] = int(tasks);
+    W.cstart[4] = int(items);
+    if (tasks >= (int64_t(1) << 30) || items >= (int64_t(1) << 30)) return false;
+    pl.o_sweep = o;
+    o = align_up(o + sizeof(float) * size_t(pfl));
+  }
+  pl.o_part = o;
+  if (env_int("GD_MSDA_SORTED_K4", 0) == 1) o = align_up(o + sizeof(float) * 128 * size_t(ncells));  // cellsum
   pl.o_scr = o;
   if (flags & GD_MSDA_DETERMINISTIC) o = align_up(o + 16 * size_t(pl.nsamples));
   pl.bytes = o;
@@ -467,12 +505,22 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
   int* cnt = reinterpret_cast<int*>(w + pl.o_cnt);
   int* off = reinterpret_cast<int*>(w + pl.o_off);
   int* bsum = reinterpret_cast<int*>(w + pl.o_bsum);
-  int* rank = reinterpret_cast<int*>(w + pl.o_rank);
+  int* cur = reinterpret_cast<int*>(w + pl.o_cur);
   int4* ids = reinterpret_cast<int4*>(w + pl.o_ids);
   int4* scr = reinterpret_cast<int4*>(w + pl.o_scr);
   float* part = reinterpret_cast<float*>(w + pl.o_part);
   const int units = pl.nsamples / 16;
   GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells), s));
+  if (units > 0) {
+    hipLaunchKernelGGL(msda_bwd_count, dim3((units + 63) / 64), dim3(256), 0, s, (const float*)loc, cnt, pl.G, Lq, M,
+                       units);
+    GD_LAUNCH_CHECK("msda_bwd_count");
+  }
+  hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);
+  hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(256), 0, s, bsum, pl.nb);
+  hipLaunchKernelGGL(scan_finish, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, (const int*)bsum, off,
+                     cur);
+  GD_LAUNCH_CHECK("msda_bwd scan");
   if (units > 0) {
     // K1 gathers one level at a time (default; fewer VGPRs: 169 vs 192 us at
     // the encoder's init geometry, 379 vs 397 us on a 2-px spread) or with
@@ -481,7 +529,7 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
 #define GD_K1(T, P)                                                                                              \
   hipLaunchKernelGGL((msda_bwd_samples<T, P>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,             \
                      (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_loc, (float*)grad_attn, \
-                     cnt, rank, pl.G, S, Lq, M, units)
+                     cur, ids, pl.G, S, Lq, M, units)
     if (dt == GD_BF16) {
       if (pipe) GD_K1(uint16_t, true); else GD_K1(uint16_t, false);
     } else {
@@ -489,15 +537,6 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
     }
 #undef GD_K1
     GD_LAUNCH_CHECK("msda_bwd_samples");
-  }
-  hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);
-  hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(256), 0, s, bsum, pl.nb);
-  hipLaunchKernelGGL(scan_finish, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, (const int*)bsum, off);
-  GD_LAUNCH_CHECK("msda_bwd scan");
-  if (units > 0) {
-    hipLaunchKernelGGL(msda_bwd_scatter, dim3((pl.nsamples + 255) / 256), dim3(256), 0, s, (const float*)loc,
-                       (const float*)attn, (const int*)off, (const int*)rank, ids, pl.G, Lq, M, pl.nsamples);
-    GD_LAUNCH_CHECK("msda_bwd_scatter");
     if (flags & GD_MSDA_DETERMINISTIC) {
       int bits = 1;
       while (bits < 31 && (int64_t(1) << bits) < pl.nsamples) ++bits;
@@ -506,6 +545,30 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       GD_LAUNCH_CHECK("msda_bwd_sort_cells");
     }
   }
+  if (env_int("GD_MSDA_SORTED_K4", 0) != 1) {
+    // K4 column sweep (+ chunk combine for the coarse levels)
+    float* sw = reinterpret_cast<float*>(w + pl.o_sweep);
+    const int sblocks = (pl.W.tstart[4] + 3) / 4;
+    const int lpu = dt == GD_BF16 ? 4 : 8;
+    const int cblocks = (pl.W.cstart[4] + 256 / lpu - 1) / (256 / lpu);
+#define GD_SW(T, TO)                                                                                          \
+  do {                                                                                                        \
+    if (sblocks > 0)                                                                                          \
+      hipLaunchKernelGGL((msda_bwd_sweep<T, TO>), dim3(sblocks), dim3(256), 0, s, (const T*)grad_out,           \
+                         (const int*)off, (const int4*)ids, (TO*)grad_value, sw, pl.G, pl.W, S, M);           \
+    GD_LAUNCH_CHECK("msda_bwd_sweep");                                                                        \
+    if (cblocks > 0)                                                                                          \
+      hipLaunchKernelGGL((msda_bwd_sweep_combine<T, TO>), dim3(cblocks), dim3(256), 0, s, (const float*)sw,   \
+                         (TO*)grad_value, pl.G, pl.W, S, M);                                                  \
+    GD_LAUNCH_CHECK("msda_bwd_sweep_combine");                                                                \
+  } while (0)
+    if (dt == GD_BF16 && gv_dt == GD_BF16) GD_SW(uint16_t, uint16_t);
+    else if (dt == GD_BF16) GD_SW(uint16_t, float);
+    else GD_SW(float, float);
+#undef GD_SW
+    return GD_OK;
+  }
+  // GD_MSDA_SORTED_K4=1: the per-cell partial + per-pixel sum pair (A/B)
   if (dt == GD_BF16)
     hipLaunchKernelGGL((msda_bwd_cellsum<uint16_t>), dim3(pl.G.cstart[4]), dim3(256), 0, s,
                        (const uint16_t*)grad_out, (const int*)off, (const int4*)ids, part, pl.G, M);

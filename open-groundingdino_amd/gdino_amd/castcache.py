@@ -139,6 +139,26 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     return F.linear(x, weight, bias)
 
 
+# GDINO_FUSED_RELU=0: the activation as its own kernel (A/B)
+FUSED_RELU = os.environ.get("GDINO_FUSED_RELU", "1") != "0"
+
+
+def linear_relu(x: torch.Tensor, layer: nn.Linear) -> torch.Tensor:
+    """F.relu(layer(x)): on the token-linear route (GPU, bf16 autocast,
+    trainable fp32 parameters) the ReLU runs in the GEMM's epilogue and its
+    backward masks by the saved output; elsewhere the plain composition."""
+    weight, bias = layer.weight, layer.bias
+    dt = autocast_dtype(x) if ENABLED else None
+    if FUSED_RELU and dt is not None and bias is not None and weight.is_floating_point():
+        params = [weight, bias]
+        route = _token_linear_ok(x, params, weight.shape[0], dt)
+        if route is not None:
+            from . import wgrad
+            return wgrad.token_linear(x, cached_cast(weight, dt), cached_cast(bias, dt), [weight], [bias],
+                                      route == "lib", relu=True)
+    return F.relu(layer(x))
+
+
 class CachedCastLinear(nn.Linear):
     """nn.Linear using cached_cast under autocast (same parameters)."""
 

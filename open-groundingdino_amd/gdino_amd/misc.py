@@ -150,6 +150,32 @@ def drop_path(x: Tensor, drop_prob: float = 0.0, training: bool = False) -> Tens
     return x * mask.div_(keep)
 
 
+def add_drop_path(x: Tensor, branch: Tensor, drop_prob: float = 0.0, training: bool = False,
+                  gamma: Optional[Tensor] = None) -> Tensor:
+    """x + drop_path(branch) (times a layer-scale ``gamma`` when given) as ONE
+    elementwise kernel: x + branch * s with s = gamma * mask / keep broadcast
+    per sample ([B, 1, C] or [B, 1, 1]) -- the residual endings of the Swin
+    blocks (swin_transformer.py:295-296) and of the BiAttention block
+    (fuse_modules.py:285-286), which the composition runs as two or three
+    passes (scale, mask multiply, add).  The per-sample mask is drawn exactly
+    as ``drop_path`` draws it (same generator call, same shape).  The add
+    runs outside autocast, whose type promotion would insert a cast kernel for
+    a bf16 branch; the kernel reads it in place and adds in fp32."""
+    s = gamma
+    if drop_prob > 0.0 and training:
+        keep = 1.0 - drop_prob
+        # in the dtype the composition's drop_path sees (gamma * branch, or
+        # the branch itself), so the mask and its 1 / keep rounding match
+        mdt = branch.dtype if gamma is None else torch.result_type(gamma, branch)
+        mask = torch.empty((branch.shape[0],) + (1,) * (branch.ndim - 1), dtype=mdt,
+                           device=branch.device).bernoulli_(keep).div_(keep)
+        s = mask if s is None else s * mask
+    if s is None:
+        return x + branch
+    with torch.autocast(device_type=x.device.type, enabled=False):
+        return torch.addcmul(x, branch, s)
+
+
 class DropPath(nn.Module):
     def __init__(self, drop_prob: float = 0.0):
         super().__init__()

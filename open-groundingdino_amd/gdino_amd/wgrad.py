@@ -143,10 +143,20 @@ class TokenLinear(torch.autograd.Function):
     matching bias blocks); gradients go to ``params`` in fp32."""
 
     @staticmethod
-    def forward(ctx, x, wc, bc, nw, lib_wgrad, *params):
+    def forward(ctx, x, wc, bc, nw, lib_wgrad, relu, *params):
         xc = x if x.dtype == wc.dtype else x.to(wc.dtype)
-        y = F.linear(xc, wc, bc)
-        ctx.save_for_backward(xc, wc)
+        if relu:
+            # relu(x wc^T + bc) in the GEMM's epilogue (hipBLASLt bias + ReLU):
+            # no separate activation pass over the [tokens, d_ffn] output;
+            # relu commutes with the bf16 rounding, so the result equals the
+            # unfused F.relu(F.linear(...))
+            y = torch._addmm_activation(bc, xc.reshape(-1, xc.shape[-1]), wc.t(), use_gelu=False)
+            y = y.view(*xc.shape[:-1], wc.shape[0])
+            ctx.save_for_backward(xc, wc, y)
+        else:
+            y = F.linear(xc, wc, bc)
+            ctx.save_for_backward(xc, wc)
+        ctx.relu = relu
         ctx.lib_wgrad = lib_wgrad
         ctx.x_dtype = x.dtype
         ctx.rows = [p.shape[0] for p in params[:nw]]
@@ -156,7 +166,11 @@ class TokenLinear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        xc, wc = ctx.saved_tensors
+        if ctx.relu:
+            xc, wc, y = ctx.saved_tensors
+            dy = torch.ops.aten.threshold_backward(dy.to(wc.dtype), y, 0)
+        else:
+            xc, wc = ctx.saved_tensors
         dy = dy.to(wc.dtype)
         dx = torch.matmul(dy, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
         i = xc.shape[-1]
@@ -165,13 +179,14 @@ class TokenLinear(torch.autograd.Function):
         grads = list(dw.split(ctx.rows, 0))
         if ctx.has_bias:
             grads += list(db.split(ctx.rows, 0))
-        return (dx, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, *grads)
 
 
-def token_linear(x, wc, bc, weights, biases, lib_wgrad=False):
+def token_linear(x, wc, bc, weights, biases, lib_wgrad=False, relu=False):
     """F.linear(x, wc, bc) whose weight / bias gradients reach the fp32
     ``weights`` / ``biases`` (row blocks of wc / bc) through the split-K
-    kernel (or, lib_wgrad, the library GEMM with fp32 output)."""
+    kernel (or, lib_wgrad, the library GEMM with fp32 output); ``relu``:
+    relu(F.linear(...)) with the activation in the GEMM epilogue."""
     params = list(weights) + (list(biases) if bc is not None else [])
     return TokenLinear.apply(x, wc.detach(), None if bc is None else bc.detach(), len(weights), bool(lib_wgrad),
-                             *params)
+                             bool(relu and bc is not None), *params)

@@ -23,7 +23,7 @@ import torch.utils.checkpoint as checkpoint
 
 from gdino_amd.conv import GemmConv2d
 from gdino_amd import castcache, kernels
-from gdino_amd.misc import DropPath, NestedTensor, to_2tuple, trunc_normal_
+from gdino_amd.misc import DropPath, NestedTensor, add_drop_path, to_2tuple, trunc_normal_
 
 
 class Mlp(nn.Module):
@@ -146,8 +146,10 @@ class SwinTransformerBlock(nn.Module):
                                                attn.relative_position_index.view(-1), mask_matrix, (h, w), ws, sh,
                                                attn.scale)
             x = attn.proj_drop(attn.proj(x))
-        x = shortcut + self.drop_path(x)
-        return x + self.drop_path(self.mlp(self.norm2(x)))
+        # x + drop_path(branch) as one kernel each (misc.add_drop_path)
+        dp = self.drop_path.drop_prob if isinstance(self.drop_path, DropPath) else 0.0
+        x = add_drop_path(shortcut, x, dp, self.training)
+        return add_drop_path(x, self.mlp(self.norm2(x)), dp, self.training)
 
     def _windowed_attention(self, x, mask_matrix):
         """reference :250-290 step by step (the path with attention dropout)"""

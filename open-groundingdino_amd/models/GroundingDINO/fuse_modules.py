@@ -13,7 +13,7 @@ import torch.nn as nn
 
 from gdino_amd import kernels
 from gdino_amd import castcache
-from gdino_amd.misc import DropPath
+from gdino_amd.misc import DropPath, add_drop_path
 
 
 class BiMultiHeadAttention(nn.Module):
@@ -81,4 +81,7 @@ class BiAttentionBlock(nn.Module):
         v = self.layer_norm_v(v)
         l = self.layer_norm_l(l)
         dv, dl = self.attn(v, l, attention_mask_v=attention_mask_v, attention_mask_l=attention_mask_l)
-        return v + self.drop_path(self.gamma_v * dv), l + self.drop_path(self.gamma_l * dl)
+        # v + drop_path(gamma_v * dv) as one kernel each (misc.add_drop_path)
+        dp = self.drop_path.drop_prob if isinstance(self.drop_path, DropPath) else 0.0
+        return (add_drop_path(v, dv, dp, self.training, self.gamma_v),
+                add_drop_path(l, dl, dp, self.training, self.gamma_l))

@@ -29,7 +29,7 @@ from gdino_amd.misc import device_const, inverse_sigmoid, topk_indices
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
 from .transformer_vanilla import TransformerEncoderLayer
-from .utils import (MLP, _get_activation_fn, _get_clones, gen_encoder_output_proposals,
+from .utils import (MLP, _get_activation_fn, _get_clones, ffn_act, gen_encoder_output_proposals,
                     gen_sineembed_for_position, get_sine_pos_embed)
 
 _DEBUG_NAN = os.environ.get("GDINO_DEBUG_NAN", "0") == "1"
@@ -360,7 +360,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
+        src2 = self.linear2(self.dropout2(ffn_act(self.linear1, self.activation, src)))
         return add_norm(self.norm2, src, self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, key_padding_mask=None):
@@ -410,7 +410,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         # the reference runs the decoder FFN outside autocast (fp32, :870-875)
         with torch.autocast(device_type=tgt.device.type, enabled=False):
             t = tgt.float() if tgt.dtype in (torch.float16, torch.bfloat16) else tgt
-            tgt2 = self.linear2(self.dropout3(self.activation(self.linear1(t))))
+            tgt2 = self.linear2(self.dropout3(ffn_act(self.linear1, self.activation, t)))
         return add_norm(self.norm3, tgt, self.dropout4(tgt2))
 
     def forward(self, tgt, tgt_query_pos=None, tgt_query_sine_embed=None, tgt_key_padding_mask=None,

@@ -135,6 +135,16 @@ def _get_activation_fn(activation, d_model=256, batch_dim=0):
     raise RuntimeError(f"activation should be relu/gelu, not {activation}.")
 
 
+def ffn_act(linear1, activation, x):
+    """activation(linear1(x)) of the FFN sublayers (reference transformer.py
+    forward_ffn, transformer_vanilla.py:83).  With ReLU on the GPU training
+    path the activation runs in the GEMM epilogue (castcache.linear_relu)."""
+    if activation is F.relu:
+        from gdino_amd.castcache import linear_relu
+        return linear_relu(x, linear1)
+    return activation(linear1(x))
+
+
 class ContrastiveEmbed(nn.Module):
     """Text-alignment logits: x . encoded_text^T, -inf on padding tokens,
     right-padded with -inf to max_text_len (reference utils.py:233-273)."""

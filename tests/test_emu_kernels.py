@@ -128,7 +128,11 @@ def _check_sorted(inputs, levels, tol, gv_dtype=torch.float32, deterministic=Fal
     (MEDIUM, 2, 37, False, 0.0, torch.float32),      # decoder shape: Lq != S, points anywhere (and outside)
     (WIDE, 1, 23, False, 0.0, torch.bfloat16),
 ])
-def test_emulated_sorted_backward_matches_oracle(levels, n, lq, local, outliers, vdtype):
+@pytest.mark.parametrize("k4", ["sweep", "cellsum"])
+def test_emulated_sorted_backward_matches_oracle(levels, n, lq, local, outliers, vdtype, k4, monkeypatch):
+    """grad_value by the column sweep (default) and by the per-cell partial +
+    per-pixel sum pair (GD_MSDA_SORTED_K4=1)."""
+    monkeypatch.setenv("GD_MSDA_SORTED_K4", "1" if k4 == "cellsum" else "0")
     S = sum(h * w for h, w in levels)
     inputs = _levels_inputs(levels, n, S if lq is None else lq, seed=11, vdtype=vdtype, local=local,
                             outlier_frac=outliers)
@@ -580,6 +584,26 @@ def test_emulated_attention(B, H, Lq, Lk, hd, mask_kind, dtype, tol, layout):
     for name, mine, r in (("dq", dq, qd.grad), ("dk", dk, kd.grad), ("dv", dv, vd.grad)):
         assert torch.isfinite(mine).all(), name
         assert E.rel_err(mine.double(), r) < tol * 2, name
+
+
+@pytest.mark.parametrize("qt,kt", [("4", "2"), ("1", "1"), ("4", "1"), ("1", "2")])
+def test_emulated_attention_wave_tilings(qt, kt, monkeypatch):
+    """Both query-tile widths of the forward / dQ kernels (64 or 16 queries
+    per wave) and both key-tile widths of the dK / dV kernel (32 or 16 keys
+    per wave), forced with GD_ATTN_QT / GD_ATTN_KT: identical math, ragged
+    lengths on both sides."""
+    from oracle.blocks import attention_ref
+    monkeypatch.setenv("GD_ATTN_QT", qt)
+    monkeypatch.setenv("GD_ATTN_KT", kt)
+    q, k, v, mask, scale, grad = _attn_case(2, 2, 150, 90, 32, "bool", torch.float32, seed=11, layout="blh")
+    out, lse = E.attn_forward(q, k, v, mask, scale)
+    qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
+    ref = attention_ref(qd, kd, vd, mask, scale)
+    assert E.rel_err(out.double(), ref.detach()) < 1e-5
+    ref.backward(grad.double())
+    dq, dk, dv = E.attn_backward(q, k, v, mask, scale, out, lse, grad)
+    for name, mine, r in (("dq", dq, qd.grad), ("dk", dk, kd.grad), ("dv", dv, vd.grad)):
+        assert E.rel_err(mine.double(), r) < 2e-5, name
 
 
 def test_emulated_attention_fully_masked_rows_are_zero():

@@ -493,6 +493,43 @@ def test_small_linear_fp32_weight_grad(t, i, o, bias):
         assert mine < 1e-2 and mine <= lib * 1.5 + 1e-6, (k, mine, lib)
 
 
+@pytest.mark.parametrize("t,i,o", [(44446, 256, 2048), (1800, 256, 2048), (512, 256, 1024)])
+def test_linear_relu_epilogue_matches_unfused(t, i, o):
+    """castcache.linear_relu (the FFN's linear1 + ReLU, the activation in the
+    GEMM epilogue; the encoder (split-K weight gradient), decoder and text
+    enhancer shapes): output bit-identical to relu of the same token-linear
+    route, gradients equal to it, both within bf16 noise of fp64."""
+    from gdino_amd import castcache
+    torch.manual_seed(t)
+    lin = torch.nn.Linear(i, o).to(DEV)
+    x = torch.randn(t, i, device=DEV)
+    gy = torch.randn(t, o, device=DEV)
+    res = {}
+    for fused in (True, False):
+        castcache.clear()
+        lin.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = (castcache.linear_relu(xi, lin) if fused else
+                 torch.relu(castcache.linear(xi, lin.weight, lin.bias)))
+        (y.float() * gy).sum().backward()
+        res[fused] = [y.float(), lin.weight.grad.clone(), lin.bias.grad.clone(), xi.grad.clone()]
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=0, atol=0)
+    for a, b in zip(res[True][1:], res[False][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    xd = x.detach().double().requires_grad_(True)
+    wd = lin.weight.detach().double().requires_grad_(True)
+    bd = lin.bias.detach().double().requires_grad_(True)
+    yd = torch.relu(torch.nn.functional.linear(xd, wd, bd))
+    (yd * gy.double()).sum().backward()
+    assert _rel(res[True][0].cpu(), yd.detach().cpu()) < 1e-2
+    # (the ReLU mask flips where bf16 and fp64 disagree on the sign of tiny
+    # pre-activations: both routes carry that error, the fused one no more)
+    for k, ref in ((1, wd.grad), (2, bd.grad), (3, xd.grad)):
+        mine, lib = _rel(res[True][k].cpu(), ref.cpu()), _rel(res[False][k].cpu(), ref.cpu())
+        assert mine <= lib * 1.05 + 1e-6, (k, mine, lib)
+
+
 # ------------------------------------------- residual add + LayerNorm (HIP)
 @pytest.mark.parametrize("shape,xd,rd", [((2, 22223, 256), torch.float32, torch.bfloat16),   # encoder, autocast
                                          ((900, 2, 256), torch.float32, torch.bfloat16),     # decoder (seq-first)

@@ -44,9 +44,48 @@ class Counter(TorchDispatchMode):
         self.by_phase = collections.Counter()
         self.phase_ops = collections.defaultdict(collections.Counter)
         self.where = collections.Counter() if "--where" in sys.argv else None
+        # --bytes: bytes touched per op (inputs + outputs) and per source line,
+        # backward ops attributed to their forward line (anomaly-mode traceback)
+        self.bytes = collections.Counter()
+        self.where_bytes = collections.Counter()
+
+    def _src(self):
+        import traceback
+        if self.phase == "backward":
+            node = torch._C._current_autograd_node()
+            tb = node.metadata.get("traceback_") if node is not None else None
+            if tb:
+                lines = "".join(tb).splitlines()
+                for i in range(len(lines) - 1, -1, -1):
+                    ln = lines[i].strip()
+                    if ln.startswith("File") and "open-groundingdino_amd" in ln and "/torch/" not in ln:
+                        f = ln.split('"')[1].split("open-groundingdino_amd/")[-1]
+                        no = ln.split("line ")[1].split(",")[0]
+                        code = lines[i + 1].strip()[:60] if i + 1 < len(lines) else ""
+                        return f"bwd {f}:{no} {code} [{type(node).__name__}]"
+                return f"bwd ? [{type(node).__name__}]"
+            return "bwd ?"
+        for fr in reversed(traceback.extract_stack()[:-2]):
+            if "open-groundingdino_amd" in fr.filename and "torch" not in fr.filename:
+                rel = fr.filename.split("open-groundingdino_amd/")[-1]
+                return f"{rel}:{fr.lineno} {fr.line.strip()[:70]}"
+        return "?"
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
+        if "--bytes" in sys.argv and not self.paused and self.phase in ("forward", "criterion", "backward"):
+            name = str(func.overloadpacket).replace("aten::", "aten.") if hasattr(func, "overloadpacket") else str(func)
+            out = func(*args, **kwargs)
+            if name not in _FREE:
+                from torch.utils._pytree import tree_leaves
+                nb = sum(t.nbytes for t in tree_leaves((args, kwargs, out)) if isinstance(t, torch.Tensor))
+                if name == "aten._to_copy":
+                    name = f"aten._to_copy[{args[0].dtype}->{kwargs.get('dtype')}]"
+                self.counts[name] += 1
+                self.bytes[name] += nb
+                if not _OP_FILTER or any(f in name for f in _OP_FILTER):
+                    self.where_bytes[self._src() + "  <" + name + ">"] += nb
+            return out
         if not self.paused:
             name = str(func.overloadpacket) if hasattr(func, "overloadpacket") else str(func)
             name = name.replace("aten::", "aten.")
@@ -75,6 +114,7 @@ def main():
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=320)
     ap.add_argument("--where", action="store_true", help="attribute fwd/criterion dispatches to source lines")
+    ap.add_argument("--bytes", action="store_true", help="bytes touched per op and per source line")
     ap.add_argument("--phase", action="store_true", help="top ops per phase")
     ap.add_argument("--op", action="append", default=[], help="with --where: only these ops (substring)")
     a = ap.parse_args()
@@ -229,7 +269,7 @@ def main():
                 kernels.override("attention", counted_attn), \
                 kernels.override("contrastive_logits", con_op), kernels.override("contrastive_rowmax", counted_rowmax):
             step(Counter())  # warm-up (caches)
-            with counter:
+            with counter, torch.autograd.set_detect_anomaly("--bytes" in sys.argv, check_nan=False):
                 step(counter)
     finally:
         msda_mod.MSDeformAttnFunction = prev
@@ -245,6 +285,14 @@ def main():
             print(f"--- {ph}")
             for k, v in c.most_common(a.top):
                 print(f"  {v:6d}  {k}")
+    if counter.bytes:
+        tot = sum(counter.bytes.values())
+        print(f"--- bytes touched (fwd + criterion + bwd): {tot / 1e9:.2f} GB")
+        for k, v in counter.bytes.most_common(a.top):
+            print(f"  {v / 1e6:10.1f} MB  {k}")
+        print("--- by source line")
+        for k, v in counter.where_bytes.most_common(a.top * 2):
+            print(f"  {v / 1e6:10.1f} MB  {k}")
     if counter.where is not None:
         print("--- forward + criterion dispatches by source line")
         for k, v in counter.where.most_common(a.top):

@@ -82,6 +82,17 @@ final)
   python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
       --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
   ;;
+benchprof)
+  # the driver's bench command, then the trace + PMC passes of the same step
+  step "bench (driver command)"
+  T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/s_bench.log 2>&1 &&
+  prof_trace s_prof --steps 3 --warmup 2 &&
+  prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&
+  prof_pmc s_pmc_write WRITE_SIZE --steps 1 --warmup 1 &&
+  step "pmc_traffic" &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
+      --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
+  ;;
 prof)
   prof_trace s_prof --steps 3 --warmup 2 &&
   prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&

@@ -191,6 +191,7 @@ def fwd_variants(iters):
 
 BWD_VARIANTS = [
     ("sorted", {"GD_MSDA_BWD": "sorted"}),
+    ("sorted cellsum", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K4": "1"}),
     ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
     ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
     ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
@@ -213,7 +214,8 @@ def bwd_variants(iters):
         ref = None
         for name, env in reversed(BWD_VARIANTS):
             saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC", "GD_MSDA_SORTED_PROBE",
-                                                    "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE")}
+                                                    "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE",
+                                                    "GD_MSDA_SORTED_K4")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
