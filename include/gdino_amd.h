@@ -60,7 +60,7 @@
  *                        nn.Linear layers (autograd's dW = dY^T X GEMM), as a
  *                        split-K fp32 reduction (no reference counterpart:
  *                        torch autograd in the reference)
- *   gd_add_layernorm_forward / _backward / _workspace_bytes
+ *   gd_add_layernorm_forward / _forward2 / _backward / _workspace_bytes
  *                     <- the post-norm `norm(src + dropout(src2))` of the
  *                        deformable encoder / decoder layers and the text
  *                        enhancer (transformer.py:789-808, 877-936,
@@ -364,8 +364,10 @@ gd_status gd_wgrad(gd_dtype dtype, const void* grad_y, int64_t ldy, const void* 
 /* ------------------------------------------------------------------------ */
 /*
  * x, r [rows, C] (F32 or BF16 each; r may be NULL), weight / bias [C] F32,
- * C in {64, 128, 192, 256, 384, 512, 768, 1024}.
+ * C in {64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048}.
  * y [rows, C] F32 = LayerNorm(x + r) * weight + bias; mean / rstd [rows] F32.
+ * _forward2 also writes y_bf16 [rows, C] BF16 = y rounded to nearest even
+ * (when not NULL): the copy a bf16 GEMM consumer would otherwise cast.
  * Backward: grad_y F32 -> grad_x (x dtype), grad_r (r dtype, or NULL),
  * grad_weight / grad_bias [C] F32 (both or neither; overwritten, need
  * gd_add_layernorm_workspace_bytes(C) bytes of workspace).  Deterministic.
@@ -374,6 +376,10 @@ size_t gd_add_layernorm_workspace_bytes(int C);
 gd_status gd_add_layernorm_forward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
                                    const float* weight, const float* bias, int64_t rows, int C,
                                    float eps, float* y, float* mean, float* rstd, gd_stream_t stream);
+gd_status gd_add_layernorm_forward2(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                    const float* weight, const float* bias, int64_t rows, int C,
+                                    float eps, float* y, void* y_bf16, float* mean, float* rstd,
+                                    gd_stream_t stream);
 gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
                                     const float* weight, const float* grad_y, const float* mean,
                                     const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,

@@ -36,27 +36,34 @@ __device__ __forceinline__ float wsum(float v) {
   return v;
 }
 
+// lane's column lane + 64 e exists (C not a multiple of 64: Swin-T's 96)
+template <int C>
+__device__ __forceinline__ bool col_ok(int lane, int e) {
+  return C % 64 == 0 || lane + 64 * e < C;
+}
+
 // grid-stride: wave w of the grid handles rows w, w + nwaves, ...
-template <typename TX, typename TR, int E>
+template <typename TX, typename TR, int C>
 __global__ void __launch_bounds__(256)
 addln_fwd_kernel(const TX* __restrict__ x, const TR* __restrict__ r, const float* __restrict__ w,
                  const float* __restrict__ b, int64_t rows, float eps, float* __restrict__ y,
-                 float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  constexpr int C = 64 * E;
+                 uint16_t* __restrict__ y16, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int E = (C + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = int64_t(gridDim.x) * 4;
   float wv[E], bv[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    wv[e] = w ? w[lane + 64 * e] : 1.f;
-    bv[e] = b ? b[lane + 64 * e] : 0.f;
+    const bool ok = col_ok<C>(lane, e);
+    wv[e] = ok && w ? w[lane + 64 * e] : 1.f;
+    bv[e] = ok && b ? b[lane + 64 * e] : 0.f;
   }
   for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
     float s[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int64_t o = row * C + lane + 64 * e;
-      s[e] = ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f);
+      s[e] = col_ok<C>(lane, e) ? ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f) : 0.f;
     }
     float sum = 0.f;
 #pragma unroll
@@ -65,12 +72,17 @@ addln_fwd_kernel(const TX* __restrict__ x, const TR* __restrict__ r, const float
     float sq = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const float d = s[e] - mean;
+      const float d = col_ok<C>(lane, e) ? s[e] - mean : 0.f;
       sq += d * d;
     }
     const float rstd = rsqrtf(wsum(sq) / float(C) + eps);
 #pragma unroll
-    for (int e = 0; e < E; ++e) y[row * C + lane + 64 * e] = (s[e] - mean) * rstd * wv[e] + bv[e];
+    for (int e = 0; e < E; ++e) {
+      if (!col_ok<C>(lane, e)) continue;
+      const float v = (s[e] - mean) * rstd * wv[e] + bv[e];
+      y[row * C + lane + 64 * e] = v;
+      if (y16) y16[row * C + lane + 64 * e] = f32_to_bf16(v);
+    }
     if (lane == 0) {
       mean_out[row] = mean;
       rstd_out[row] = rstd;
@@ -79,20 +91,20 @@ addln_fwd_kernel(const TX* __restrict__ x, const TR* __restrict__ r, const float
 }
 
 // dy [rows, C] fp32 -> dx (TX), dr (TR, optional), partial dw / db per wave
-template <typename TX, typename TR, int E>
+template <typename TX, typename TR, int C>
 __global__ void __launch_bounds__(256)
 addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const TR* __restrict__ r,
                  const float* __restrict__ w, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                  int64_t rows, TX* __restrict__ dx, TR* __restrict__ dr, float* __restrict__ part_w,
                  float* __restrict__ part_b) {
-  constexpr int C = 64 * E;
+  constexpr int E = (C + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int64_t wave_id = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = int64_t(gridDim.x) * 4;
   float wv[E], gw[E], gb[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    wv[e] = w ? w[lane + 64 * e] : 1.f;
+    wv[e] = col_ok<C>(lane, e) && w ? w[lane + 64 * e] : 1.f;
     gw[e] = gb[e] = 0.f;
   }
   for (int64_t row = wave_id; row < rows; row += nwaves) {
@@ -102,9 +114,10 @@ addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const T
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int64_t o = row * C + lane + 64 * e;
-      const float s = ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f);
-      xh[e] = (s - mean) * rstd;
-      const float d = dy[o];
+      const bool ok = col_ok<C>(lane, e);
+      const float s = ok ? ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f) : 0.f;
+      xh[e] = ok ? (s - mean) * rstd : 0.f;
+      const float d = ok ? dy[o] : 0.f;
       gw[e] += d * xh[e];
       gb[e] += d;
       g[e] = d * wv[e];
@@ -114,6 +127,7 @@ addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const T
     const float mg = wsum(sg) / float(C), mgx = wsum(sgx) / float(C);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
+      if (!col_ok<C>(lane, e)) continue;
       const int64_t o = row * C + lane + 64 * e;
       const float ds = rstd * (g[e] - mg - xh[e] * mgx);
       stv<TX>(dx + o, ds);
@@ -125,6 +139,7 @@ addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const T
     const int wv_i = threadIdx.x >> 6;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
+      if (!col_ok<C>(lane, e)) continue;
       red[0][wv_i][lane + 64 * e] = gw[e];
       red[1][wv_i][lane + 64 * e] = gb[e];
     }
@@ -173,20 +188,24 @@ template <typename Fn>
 gd_status dispatch_types(gd_dtype tx, gd_dtype tr, bool has_r, int C, Fn&& fn) {
   GD_REQUIRE(tx == GD_F32 || tx == GD_BF16, "add_layernorm: x dtype %d (F32, BF16)", int(tx));
   GD_REQUIRE(!has_r || tr == GD_F32 || tr == GD_BF16, "add_layernorm: r dtype %d (F32, BF16)", int(tr));
-  GD_REQUIRE(C == 64 || C == 128 || C == 192 || C == 256 || C == 384 || C == 512 || C == 768 || C == 1024,
-             "add_layernorm: C=%d not supported (64, 128, 192, 256, 384, 512, 768, 1024)", C);
+  GD_REQUIRE(C == 64 || C == 96 || C == 128 || C == 192 || C == 256 || C == 384 || C == 512 || C == 768 ||
+                 C == 1024 || C == 1536 || C == 2048,
+             "add_layernorm: C=%d not supported (64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048)", C);
   auto with_e = [&](auto tx_tag, auto tr_tag) {
     using TX = decltype(tx_tag);
     using TR = decltype(tr_tag);
     switch (C) {
-      case 64: fn(TX{}, TR{}, std::integral_constant<int, 1>{}); break;
-      case 128: fn(TX{}, TR{}, std::integral_constant<int, 2>{}); break;
-      case 192: fn(TX{}, TR{}, std::integral_constant<int, 3>{}); break;
-      case 256: fn(TX{}, TR{}, std::integral_constant<int, 4>{}); break;
-      case 384: fn(TX{}, TR{}, std::integral_constant<int, 6>{}); break;
-      case 512: fn(TX{}, TR{}, std::integral_constant<int, 8>{}); break;
-      case 768: fn(TX{}, TR{}, std::integral_constant<int, 12>{}); break;
-      default: fn(TX{}, TR{}, std::integral_constant<int, 16>{}); break;
+      case 64: fn(TX{}, TR{}, std::integral_constant<int, 64>{}); break;
+      case 96: fn(TX{}, TR{}, std::integral_constant<int, 96>{}); break;
+      case 128: fn(TX{}, TR{}, std::integral_constant<int, 128>{}); break;
+      case 192: fn(TX{}, TR{}, std::integral_constant<int, 192>{}); break;
+      case 256: fn(TX{}, TR{}, std::integral_constant<int, 256>{}); break;
+      case 384: fn(TX{}, TR{}, std::integral_constant<int, 384>{}); break;
+      case 512: fn(TX{}, TR{}, std::integral_constant<int, 512>{}); break;
+      case 768: fn(TX{}, TR{}, std::integral_constant<int, 768>{}); break;
+      case 1024: fn(TX{}, TR{}, std::integral_constant<int, 1024>{}); break;
+      case 1536: fn(TX{}, TR{}, std::integral_constant<int, 1536>{}); break;
+      default: fn(TX{}, TR{}, std::integral_constant<int, 2048>{}); break;
     }
   };
   const bool xb = tx == GD_BF16, rb = has_r && tr == GD_BF16;
@@ -207,6 +226,14 @@ extern "C" size_t gd_add_layernorm_workspace_bytes(int C) { return sizeof(float)
 extern "C" gd_status gd_add_layernorm_forward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
                                              const float* weight, const float* bias, int64_t rows, int C,
                                              float eps, float* y, float* mean, float* rstd, gd_stream_t stream) {
+  return gd_add_layernorm_forward2(x_dtype, x, r_dtype, r, weight, bias, rows, C, eps, y, nullptr, mean, rstd,
+                                   stream);
+}
+
+extern "C" gd_status gd_add_layernorm_forward2(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                              const float* weight, const float* bias, int64_t rows, int C,
+                                              float eps, float* y, void* y_bf16, float* mean, float* rstd,
+                                              gd_stream_t stream) {
   GD_REQUIRE(rows >= 0, "add_layernorm: rows < 0");
   if (rows == 0) return gd_status(GD_OK);
   GD_REQUIRE(x && y && mean && rstd, "add_layernorm_forward: null pointer");
@@ -217,7 +244,7 @@ extern "C" gd_status gd_add_layernorm_forward(gd_dtype x_dtype, const void* x, g
     using TX = decltype(tx);
     using TR = decltype(tr);
     hipLaunchKernelGGL((addln_fwd_kernel<TX, TR, decltype(e)::value>), dim3(blocks), dim3(256), 0, s,
-                       (const TX*)x, (const TR*)r, weight, bias, rows, eps, y, mean, rstd);
+                       (const TX*)x, (const TR*)r, weight, bias, rows, eps, y, (uint16_t*)y_bf16, mean, rstd);
   });
   if (st != GD_OK) return st;
   GD_LAUNCH_CHECK("add_layernorm_fwd");

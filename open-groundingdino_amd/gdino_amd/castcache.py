@@ -195,6 +195,25 @@ def _cached_cat(params, dtype):
     return t
 
 
+def linear_shared_input_joint(x: torch.Tensor, layers):
+    """The one-GEMM output of ``linear_shared_input`` left unsplit ([..., sum
+    of out_features], the layers' outputs side by side), or None when the
+    fused route does not apply.  A consumer that reads the column blocks in
+    place (biattn.BiAttnTokens) then hands back ONE gradient tensor: no
+    split backward's concatenation of the blocks' gradients."""
+    dt = autocast_dtype(x)
+    if dt is None or not FUSE_SHARED_INPUT or any(m.bias is None for m in layers):
+        return None
+    w = _cached_cat([m.weight for m in layers], dt)
+    b = _cached_cat([m.bias for m in layers], dt)
+    params = [m.weight for m in layers] + [m.bias for m in layers]
+    route = _token_linear_ok(x, params, w.shape[0], dt)
+    if route is None:
+        return None
+    from . import wgrad
+    return wgrad.token_linear(x, w, b, [m.weight for m in layers], [m.bias for m in layers], route == "lib")
+
+
 def linear_shared_input(x: torch.Tensor, layers):
     """[layer(x) for layer in layers] for nn.Linear layers reading the same
     input.  Under autocast with the cache on, one GEMM against the cached

@@ -21,19 +21,32 @@ from . import _lib
 
 _p, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _lib.register("gd_add_layernorm_forward", [_i, _p, _i, _p, _p, _p, _i64, _i, _f, _p, _p, _p, _p])
+_lib.register("gd_add_layernorm_forward2", [_i, _p, _i, _p, _p, _p, _i64, _i, _f, _p, _p, _p, _p, _p])
+
+
+def _bf16_twin_wanted(x) -> bool:
+    """Under bf16 autocast the fp32 LayerNorm output is cast again by every
+    GEMM that reads it; the forward kernel writes that bf16 copy itself
+    (``y._gd_bf16``, read by wgrad.TokenLinear) for one extra 2-byte store
+    per element instead of a cast kernel per consumer."""
+    return (TWIN and x.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+TWIN = True
 _lib.register("gd_add_layernorm_backward", [_i, _p, _i, _p, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p])
 
-WIDTHS = (64, 128, 192, 256, 384, 512, 768, 1024)
+WIDTHS = (64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048)
 ENABLED = True
 
 
-def supported(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor) -> bool:
+def supported(norm: nn.LayerNorm, x: torch.Tensor, r) -> bool:
     c = x.shape[-1]
     return (ENABLED and _lib.enabled("addln") and _lib.on_device(x) and len(norm.normalized_shape) == 1
             and norm.normalized_shape[0] == c and c in WIDTHS and norm.elementwise_affine and norm.weight is not None and norm.bias is not None
             and norm.weight.dtype == torch.float32 and norm.bias.dtype == torch.float32
-            and x.dtype in (torch.float32, torch.bfloat16) and r.dtype in (torch.float32, torch.bfloat16)
-            and x.shape == r.shape)
+            and x.dtype in (torch.float32, torch.bfloat16)
+            and (r is None or (r.dtype in (torch.float32, torch.bfloat16) and x.shape == r.shape)))
 
 
 def _workspace(c, device):
@@ -50,10 +63,15 @@ class AddLayerNormFunction(torch.autograd.Function):
         y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         mean = torch.empty(rows, dtype=torch.float32, device=x.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-        _lib.call("gd_add_layernorm_forward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(r), r.data_ptr(),
-                  weight.data_ptr(), bias.data_ptr(), rows, c, float(eps), y.data_ptr(), mean.data_ptr(),
-                  rstd.data_ptr(), _lib.stream_of(x),
-                  nbytes=rows * (c * (x.element_size() + r.element_size() + 4) + 8))  # x, r -> y, mean, rstd
+        rd = x if r is None else r  # r None: LayerNorm(x) alone (NULL residual)
+        y16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if _bf16_twin_wanted(x) else None
+        _lib.call("gd_add_layernorm_forward2", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(rd), _lib.ptr(r),
+                  weight.data_ptr(), bias.data_ptr(), rows, c, float(eps), y.data_ptr(), _lib.ptr(y16),
+                  mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(x),
+                  nbytes=rows * (c * (x.element_size() + (0 if r is None else r.element_size()) + 4
+                                      + (0 if y16 is None else 2)) + 8))
+        if y16 is not None:
+            y._gd_bf16 = (y16, y._version)  # stale once y is modified in place
         ctx.save_for_backward(x, r, weight, mean, rstd)
         return y
 
@@ -64,18 +82,28 @@ class AddLayerNormFunction(torch.autograd.Function):
         rows = x.numel() // c
         dy = dy.float().contiguous()
         dx = torch.empty_like(x)
-        dr = torch.empty_like(r) if ctx.needs_input_grad[1] else None
+        dr = torch.empty_like(r) if r is not None and ctx.needs_input_grad[1] else None
         want_wb = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         dw = torch.empty(c, dtype=torch.float32, device=x.device) if want_wb else None
         db = torch.empty(c, dtype=torch.float32, device=x.device) if want_wb else None
         ws = _workspace(c, x.device) if want_wb else None
-        _lib.call("gd_add_layernorm_backward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(r), r.data_ptr(),
+        _lib.call("gd_add_layernorm_backward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(x if r is None else r),
+                  _lib.ptr(r),
                   weight.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, c, dx.data_ptr(),
                   _lib.ptr(dr), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws), _lib.stream_of(x),
-                  nbytes=rows * (c * (2 * x.element_size() + r.element_size() + 4
+                  nbytes=rows * (c * (2 * x.element_size() + (0 if r is None else r.element_size()) + 4
                                       + (r.element_size() if dr is not None else 0)) + 8))
         return (dx if ctx.needs_input_grad[0] else None, dr, dw if ctx.needs_input_grad[2] else None,
                 db if ctx.needs_input_grad[3] else None, None)
+
+
+def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+    """norm(x) with no residual (Swin's pre-norms and patch-merging norm,
+    swin_transformer.py:245, 296, 357): the same kernels with a NULL residual,
+    fp32 output as autocast's LayerNorm; elsewhere nn.LayerNorm."""
+    if supported(norm, x, None):
+        return AddLayerNormFunction.apply(x.contiguous(), None, norm.weight, norm.bias, norm.eps)
+    return norm(x)
 
 
 def add_norm(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor) -> torch.Tensor:

@@ -137,6 +137,21 @@ def tn_matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return out.reshape(*lead, o, i)
 
 
+def _dx(dy, wc, x_dtype):
+    """dX = dY . W for an fp32 input: the library GEMM writes fp32 directly
+    (aten::mm.dtype, fp32 accumulation) instead of a bf16 result plus a
+    cast kernel; other dtypes, or a torch without mm.dtype, the plain
+    product."""
+    global _MM_DTYPE_OK
+    if x_dtype == torch.float32 and dy.dtype == torch.bfloat16 and _MM_DTYPE_OK and dy.is_cuda:
+        try:
+            return torch.mm(dy.reshape(-1, dy.shape[-1]), wc, out_dtype=torch.float32).view(*dy.shape[:-1],
+                                                                                         wc.shape[-1])
+        except (RuntimeError, NotImplementedError, TypeError):
+            _MM_DTYPE_OK = False
+    return torch.matmul(dy, wc).to(x_dtype)
+
+
 class TokenLinear(torch.autograd.Function):
     """y = x . wc^T + bc with wc / bc the low-precision copies of the fp32
     parameters ``params`` (one or several row blocks of the weight, then the
@@ -144,7 +159,13 @@ class TokenLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wc, bc, nw, lib_wgrad, relu, *params):
-        xc = x if x.dtype == wc.dtype else x.to(wc.dtype)
+        # the bf16 copy a producer wrote beside x (layernorm: ``_gd_bf16``)
+        # instead of a cast kernel
+        tw = getattr(x, "_gd_bf16", None)
+        if tw is not None and tw[1] == x._version and tw[0].dtype == wc.dtype and tw[0].shape == x.shape:
+            xc = tw[0]
+        else:
+            xc = x if x.dtype == wc.dtype else x.to(wc.dtype)
         if relu:
             # relu(x wc^T + bc) in the GEMM's epilogue (hipBLASLt bias + ReLU):
             # no separate activation pass over the [tokens, d_ffn] output;
@@ -172,7 +193,7 @@ class TokenLinear(torch.autograd.Function):
         else:
             xc, wc = ctx.saved_tensors
         dy = dy.to(wc.dtype)
-        dx = torch.matmul(dy, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+        dx = _dx(dy, wc, ctx.x_dtype) if ctx.needs_input_grad[0] else None
         i = xc.shape[-1]
         wg = weight_grad_lib if ctx.lib_wgrad else weight_grad
         dw, db = wg(dy.reshape(-1, dy.shape[-1]).contiguous(), xc.reshape(-1, i).contiguous(), ctx.has_bias)

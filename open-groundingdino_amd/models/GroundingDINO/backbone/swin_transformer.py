@@ -23,6 +23,7 @@ import torch.utils.checkpoint as checkpoint
 
 from gdino_amd.conv import GemmConv2d
 from gdino_amd import castcache, kernels
+from gdino_amd.layernorm import layer_norm
 from gdino_amd.misc import DropPath, NestedTensor, add_drop_path, to_2tuple, trunc_normal_
 
 
@@ -133,7 +134,7 @@ class SwinTransformerBlock(nn.Module):
         assert length == h * w, "input feature has wrong size"
         ws, sh = self.window_size, self.shift_size
         shortcut = x
-        x = self.norm1(x)
+        x = layer_norm(self.norm1, x)
         attn = self.attn
         if attn.attn_drop.p > 0.0 and self.training:
             x = self._windowed_attention(x, mask_matrix)
@@ -149,7 +150,7 @@ class SwinTransformerBlock(nn.Module):
         # x + drop_path(branch) as one kernel each (misc.add_drop_path)
         dp = self.drop_path.drop_prob if isinstance(self.drop_path, DropPath) else 0.0
         x = add_drop_path(shortcut, x, dp, self.training)
-        return add_drop_path(x, self.mlp(self.norm2(x)), dp, self.training)
+        return add_drop_path(x, self.mlp(layer_norm(self.norm2, x)), dp, self.training)
 
     def _windowed_attention(self, x, mask_matrix):
         """reference :250-290 step by step (the path with attention dropout)"""
@@ -194,7 +195,7 @@ class PatchMerging(nn.Module):
             x = F.pad(x, (0, 0, 0, w % 2, 0, h % 2))
         # channel order (x0, x1, x2, x3) = (even,even), (odd,even), (even,odd), (odd,odd)
         x = torch.cat([x[:, 0::2, 0::2], x[:, 1::2, 0::2], x[:, 0::2, 1::2], x[:, 1::2, 1::2]], -1)
-        return self.reduction(self.norm(x.view(b, -1, 4 * c)))
+        return self.reduction(layer_norm(self.norm, x.view(b, -1, 4 * c)))
 
 
 _MASK_CACHE: Dict[Tuple, torch.Tensor] = {}
@@ -343,7 +344,7 @@ class SwinTransformer(nn.Module):
         for i, layer in enumerate(self.layers):
             x_out, h, w, x, wh, ww = layer(x, wh, ww)
             if i in self.out_indices:
-                y = getattr(self, f"norm{i}")(x_out)
+                y = layer_norm(getattr(self, f"norm{i}"), x_out)
                 outs.append(y.view(-1, h, w, self.num_features[i]).permute(0, 3, 1, 2).contiguous())
         return outs
 

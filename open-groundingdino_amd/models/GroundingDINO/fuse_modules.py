@@ -11,8 +11,9 @@ pre-LayerNorms, layer-scale gammas (init 1e-4) and DropPath as the reference.
 import torch
 import torch.nn as nn
 
-from gdino_amd import kernels
+from gdino_amd import biattn, kernels
 from gdino_amd import castcache
+from gdino_amd.layernorm import layer_norm
 from gdino_amd.misc import DropPath, add_drop_path
 
 
@@ -54,11 +55,28 @@ class BiMultiHeadAttention(nn.Module):
         b, s, _ = v.shape
         t = l.shape[1]
         # projections sharing an input run as one GEMM on the training path
-        qv, vv = castcache.linear_shared_input(v, (self.v_proj, self.values_v_proj))
-        kl, vl = castcache.linear_shared_input(l, (self.l_proj, self.values_l_proj))
+        p = self.dropout if self.training else 0.0
+        if p == 0.0:
+            # token-major core (gdino_amd/biattn.py) on the joint projection
+            # outputs: no head-split copies, no split / concatenation
+            qvv = castcache.linear_shared_input_joint(v, (self.v_proj, self.values_v_proj))
+            klv = castcache.linear_shared_input_joint(l, (self.l_proj, self.values_l_proj))
+            if biattn.tokens_ok(qvv, klv, self.num_heads):
+                out_v, out_l = biattn.bi_attention_tokens(qvv, klv, attention_mask_v, attention_mask_l,
+                                                          self.num_heads, self.scale)
+                return self.out_v_proj(out_v), self.out_l_proj(out_l)
+            if qvv is not None and klv is not None:
+                from gdino_amd.misc import split_last
+                qv, vv = split_last(qvv, [self.embed_dim, self.embed_dim])
+                kl, vl = split_last(klv, [self.embed_dim, self.embed_dim])
+            else:
+                qv, vv = castcache.linear_shared_input(v, (self.v_proj, self.values_v_proj))
+                kl, vl = castcache.linear_shared_input(l, (self.l_proj, self.values_l_proj))
+        else:
+            qv, vv = castcache.linear_shared_input(v, (self.v_proj, self.values_v_proj))
+            kl, vl = castcache.linear_shared_input(l, (self.l_proj, self.values_l_proj))
         q = self._heads(qv * self.scale)
         k, vv, vl = self._heads(kl), self._heads(vv), self._heads(vl)
-        p = self.dropout if self.training else 0.0
         out_v, out_l = kernels.bi_attention(q, k, vv, vl, attention_mask_v, attention_mask_l, p)
         out_v = out_v.transpose(1, 2).reshape(b, s, self.embed_dim)
         out_l = out_l.transpose(1, 2).reshape(b, t, self.embed_dim)
@@ -78,8 +96,8 @@ class BiAttentionBlock(nn.Module):
         self.gamma_l = nn.Parameter(init_values * torch.ones(l_dim), requires_grad=True)
 
     def forward(self, v, l, attention_mask_v=None, attention_mask_l=None):
-        v = self.layer_norm_v(v)
-        l = self.layer_norm_l(l)
+        v = layer_norm(self.layer_norm_v, v)  # HIP LayerNorm (+ bf16 copy for the projections)
+        l = layer_norm(self.layer_norm_l, l)
         dv, dl = self.attn(v, l, attention_mask_v=attention_mask_v, attention_mask_l=attention_mask_l)
         # v + drop_path(gamma_v * dv) as one kernel each (misc.add_drop_path)
         dp = self.drop_path.drop_prob if isinstance(self.drop_path, DropPath) else 0.0

@@ -731,15 +731,18 @@ def test_emulated_wgrad(T, O, I, splits, dtype, tol):
     (50, 192, torch.float32, torch.float32),
     (9, 768, torch.bfloat16, torch.bfloat16),
     (3000, 64, torch.float32, torch.float32),   # more rows than the backward grid's waves
+    (41, 96, torch.float32, None),              # Swin-T stage 0: C not a multiple of 64, no residual
+    (7, 1536, torch.bfloat16, None),            # patch-merging width, no residual
+    (5, 2048, torch.float32, torch.bfloat16),
 ])
 def test_emulated_add_layernorm(rows, C, xd, rd):
     g = torch.Generator().manual_seed(rows + C)
     x = (torch.randn(rows, C, generator=g) * 2 + 0.5).to(xd)
-    r = torch.randn(rows, C, generator=g).to(rd)
+    r = torch.randn(rows, C, generator=g).to(rd) if rd is not None else None
     w = torch.randn(C, generator=g)
     b = torch.randn(C, generator=g)
     y, mean, rstd = E.add_layernorm_forward(x, r, w, b, 1e-5)
-    xs = (x.double() + r.double()).requires_grad_(True)
+    xs = (x.double() + (r.double() if r is not None else 0)).requires_grad_(True)
     wd, bd = w.double().requires_grad_(True), b.double().requires_grad_(True)
     ref = torch.nn.functional.layer_norm(xs, (C,), wd, bd, 1e-5)
     assert E.rel_err(y, ref.detach()) < 1e-5
@@ -748,6 +751,9 @@ def test_emulated_add_layernorm(rows, C, xd, rd):
     dx, dr, dw, db = E.add_layernorm_backward(x, r, w, dy, mean, rstd)
     tol = 1e-5 if xd == torch.float32 else 1e-2
     assert E.rel_err(dx.double(), xs.grad) < tol
-    assert E.rel_err(dr.double(), xs.grad) < (1e-5 if rd == torch.float32 else 1e-2)
+    if r is not None:
+        assert E.rel_err(dr.double(), xs.grad) < (1e-5 if rd == torch.float32 else 1e-2)
+    else:
+        assert dr is None
     assert E.rel_err(dw, wd.grad) < 1e-5
     assert E.rel_err(db, bd.grad) < 1e-5

@@ -79,6 +79,39 @@ def test_bi_attention_production_shape_bf16():
     assert _rel(ol, rl) < 1e-2
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("shape", [(2, 4, 300, 40, 64), (2, 4, 5000, 256, 256), (2, 4, 22223, 256, 256)])
+def test_bi_attention_tokens_matches_head_path(dtype, tol, shape):
+    """The token-major core (biattn.BiAttnTokens: strided per-head GEMM views
+    of the joint projection outputs (q | v_v) [B, S, 2E] and (k | v_l)
+    [B, T, 2E], the score scale on k, one gradient tensor per joint output)
+    against the head-major path with the scale on q: outputs and gradients."""
+    from gdino_amd.biattn import BiAttnTokens, bi_attention_hip, tokens_ok
+    b, h, s, t, hd = shape
+    (q, k, vv, vl), pad_v, pad_l = _bi_inputs(b, h, s, t, hd, dtype, seed=5)
+    e, scale = h * hd, 0.5
+    tok = lambda x: x.transpose(1, 2).reshape(x.shape[0], x.shape[2], e)  # noqa: E731
+    qvv = torch.cat([tok(q), tok(vv)], -1).to(DEV)
+    klv = torch.cat([tok(k), tok(vl)], -1).to(DEV)
+    gv = torch.randn(b, s, e, device=DEV).to(dtype)
+    gl = torch.randn(b, t, e, device=DEV).to(dtype)
+    res = []
+    for path in ("tokens", "heads"):
+        qvv_, klv_ = qvv.clone().requires_grad_(True), klv.clone().requires_grad_(True)
+        if path == "tokens":
+            assert tokens_ok(qvv_, klv_, h)
+            ov, ol = BiAttnTokens.apply(qvv_, klv_, pad_v.to(DEV), pad_l.to(DEV), h, scale)
+        else:
+            hv = lambda x: x.unflatten(-1, (h, hd)).transpose(1, 2)  # noqa: E731
+            ov, ol = bi_attention_hip(hv(qvv_[..., :e] * scale), hv(klv_[..., :e]), hv(qvv_[..., e:]),
+                                      hv(klv_[..., e:]), pad_v.to(DEV), pad_l.to(DEV), 0.0)
+            ov, ol = tok(ov), tok(ol)
+        ((ov.float() * gv.float()).sum() + (ol.float() * gl.float()).sum()).backward()
+        res.append([ov.float(), ol.float(), qvv_.grad.float(), klv_.grad.float()])
+    for name, a, r in zip(("out_v", "out_l", "d(q | vv)", "d(k | vl)"), *res):
+        assert _rel(a, r) < tol, name
+
+
 # --------------------------------------------- Swin window attention (HIP)
 def _wattn_inputs(ws, nh, b_, nw, masked, dtype, seed=0):
     from models.GroundingDINO.backbone.swin_transformer import relative_position_index
@@ -560,6 +593,70 @@ def test_add_layernorm_matches_reference(shape, xd, rd):
     assert _rel(rg.grad.cpu(), rd64.grad) < (1e-2 if rd == torch.bfloat16 else 1e-5)
     assert _rel(norm.weight.grad.cpu(), wd.grad) < 1e-5
     assert _rel(norm.bias.grad.cpu(), bd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("shape,xd", [((2, 66800, 96), torch.float32),    # Swin-T stage 0 (C not a multiple of 64)
+                                      ((2, 4200, 1536), torch.float32),    # stage-2 patch merging (4 x 384)
+                                      ((2, 16700, 192), torch.bfloat16),
+                                      ((3, 77, 2048), torch.float32)])     # Swin-B merging width
+def test_layer_norm_no_residual_matches_reference(shape, xd):
+    """layernorm.layer_norm (the add + LayerNorm kernels with a NULL
+    residual): Swin's pre-norms, patch-merging and output norms."""
+    from gdino_amd.layernorm import layer_norm
+    g = torch.Generator().manual_seed(shape[-1])
+    c = shape[-1]
+    norm = torch.nn.LayerNorm(c).to(DEV)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(c, generator=g))
+        norm.bias.copy_(torch.randn(c, generator=g))
+    x = (torch.randn(shape, generator=g) * 2 + 0.5).to(xd)
+    dy = torch.randn(shape, generator=g)
+    xg = x.to(DEV).requires_grad_(True)
+    y = layer_norm(norm, xg)
+    assert y.dtype == torch.float32 and "AddLayerNorm" in type(y.grad_fn).__name__
+    y.backward(dy.to(DEV))
+    xd64 = x.detach().double().requires_grad_(True)
+    wd = norm.weight.detach().double().cpu().requires_grad_(True)
+    bd = norm.bias.detach().double().cpu().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xd64, (c,), wd, bd, norm.eps)
+    ref.backward(dy.double())
+    assert _rel(y.detach().cpu(), ref.detach()) < 1e-5
+    assert _rel(xg.grad.cpu(), xd64.grad) < (1e-2 if xd == torch.bfloat16 else 1e-5)
+    assert _rel(norm.weight.grad.cpu(), wd.grad) < 1e-5
+    assert _rel(norm.bias.grad.cpu(), bd.grad) < 1e-5
+
+
+def test_layer_norm_bf16_twin_feeds_token_linear():
+    """Under bf16 autocast the LayerNorm kernel also writes its output's bf16
+    copy (y._gd_bf16) and TokenLinear reads it instead of casting: equal to
+    the cast, and the Linear's output and every gradient identical to the
+    path that casts (a clone carries no copy)."""
+    from gdino_amd import castcache
+    from gdino_amd.layernorm import layer_norm
+    torch.manual_seed(0)
+    norm = torch.nn.LayerNorm(256).to(DEV)
+    lin = torch.nn.Linear(256, 512).to(DEV)
+    x = torch.randn(2, 5000, 256, device=DEV)
+    gy = torch.randn(2, 5000, 512, device=DEV)
+    res = []
+    for twin in (True, False):
+        castcache.clear()
+        lin.zero_grad()
+        norm.zero_grad()
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = layer_norm(norm, xi)
+            if twin:
+                t16, ver = y._gd_bf16
+                assert ver == y._version and torch.equal(t16, y.to(torch.bfloat16))
+            else:
+                y = y.clone()
+                assert getattr(y, "_gd_bf16", None) is None
+            out = castcache.linear(y, lin.weight, lin.bias)
+        (out.float() * gy).sum().backward()
+        res.append([out.float(), xi.grad, lin.weight.grad.clone(), norm.weight.grad.clone()])
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
 def test_tn_matmul_biattention_shape():

@@ -225,7 +225,8 @@ def main():
     # residual add + LayerNorm (GPU-only, gdino_amd/layernorm.py): one
     # launch forward, two backward (kernel + column reduction)
     from gdino_amd import layernorm as ln_mod
-    ln_op = counted(lambda x, r, w, b, eps: torch.nn.functional.layer_norm(x.float() + r.float(), w.shape, w, b, eps),
+    ln_op = counted(lambda x, r, w, b, eps: torch.nn.functional.layer_norm(
+        x.float() + (0 if r is None else r.float()), w.shape, w, b, eps),
                     "gd.add_layernorm")
 
     class CountedAddLN:

@@ -19,7 +19,10 @@ PEAK = 2.5e15
 SHAPES = [("enc value/output proj", 44446, 256, 256), ("enc offsets+weights", 44446, 384, 256),
           ("enc ffn1", 44446, 2048, 256), ("enc ffn2", 44446, 256, 2048),
           ("swin0 qkv", 133600, 288, 96), ("swin0 fc1", 133600, 384, 96), ("swin0 fc2", 133600, 96, 384),
-          ("swin1 qkv", 33400, 576, 192), ("swin1 fc1", 33400, 768, 192), ("swin2 fc1", 8350, 1536, 384)]
+          ("swin1 qkv", 33400, 576, 192), ("swin1 fc1", 33400, 768, 192), ("swin2 fc1", 8350, 1536, 384),
+          # below the split-K threshold today (library GEMM + fp32 sum): decoder (1 800 query tokens), text (512)
+          ("dec proj", 1800, 256, 256), ("dec offsets+weights", 1800, 384, 256), ("dec ffn1", 1800, 2048, 256),
+          ("dec ffn2", 1800, 256, 2048), ("text proj", 512, 256, 256), ("text ffn1", 512, 1024, 256)]
 
 
 def time_it(fn, iters=20, warm=3):
@@ -45,7 +48,7 @@ def main():
         x = torch.randn(t, i, generator=g, device="cuda").to(torch.bfloat16)
         flops = 2.0 * t * o * i
         mine = time_it(lambda: wgrad.weight_grad(dy, x, True), a.iters)
-        lib = time_it(lambda: (torch.mm(dy.t(), x), dy.sum(0)), a.iters)
+        lib = time_it(lambda: wgrad.weight_grad_lib(dy, x, True), a.iters)  # bf16 x bf16 -> fp32 GEMM + fp32 sum
         dw, db = wgrad.weight_grad(dy, x, True)
         ref = dy.double().t() @ x.double()
         err = float((dw.double() - ref).abs().max() / ref.abs().max())
