@@ -451,7 +451,7 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
       W.bands[l] = (Wd + gpw - 2) / (gpw - 1);
       W.rblk[l] = (H + R - 1) / R;
       W.tstart[l] = int(tasks);
-      tasks += int64_t(N) * M * W.bands[l] * W.rblk[l] * Gs;
+      tasks += int64_t(W.bands[l]) * W.rblk[l] * Gs;  // per (n, m)
       W.cstart[l] = int(items);
       W.pbase[l] = pfl;
       if (Gs > 1) {
@@ -461,7 +461,8 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
     }
     W.tstart[4] = int(tasks);
     W.cstart[4] = int(items);
-    if (tasks >= (int64_t(1) << 30) || items >= (int64_t(1) << 30)) return false;
+    if (tasks * N * M >= (int64_t(1) << 30) || items >= (int64_t(1) << 30)) return false;
+    W.ntasks = int(tasks * N * M);
     pl.o_sweep = o;
     o = align_up(o + sizeof(float) * size_t(pfl));
   }
@@ -532,6 +533,19 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
     // the encoder's init geometry, 379 vs 397 us on a 2-px spread) or with
     // the next level in flight (GD_MSDA_SORTED_K1PIPE=1)
     const bool pipe = env_int("GD_MSDA_SORTED_K1PIPE", 0) != 0;
+    // GD_MSDA_SORTED_K1=2: the level-by-level variant (103 VGPRs, 4 waves
+    // per SIMD; measured 380 vs 367 us at the init geometry, 846 vs 884 on
+    // a 2-px spread -- twice the waves in flight double its L2 misses)
+    if (env_int("GD_MSDA_SORTED_K1", 1) == 2) {
+      if (dt == GD_BF16)
+        hipLaunchKernelGGL((msda_bwd_samples_lv<uint16_t>), dim3(pl.k1_blocks), dim3(256), 0, s,
+                           (const uint16_t*)value, (const float*)loc, (const float*)attn, (const uint16_t*)grad_out,
+                           (float*)grad_loc, (float*)grad_attn, cur, ids, pl.G, S, Lq, M, units);
+      else
+        hipLaunchKernelGGL((msda_bwd_samples_lv<float>), dim3(pl.k1_blocks), dim3(256), 0, s, (const float*)value,
+                           (const float*)loc, (const float*)attn, (const float*)grad_out, (float*)grad_loc,
+                           (float*)grad_attn, cur, ids, pl.G, S, Lq, M, units);
+    } else {
 #define GD_K1(T, P)                                                                                              \
   hipLaunchKernelGGL((msda_bwd_samples<T, P>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,             \
                      (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_loc, (float*)grad_attn, \
@@ -542,6 +556,7 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       if (pipe) GD_K1(float, true); else GD_K1(float, false);
     }
 #undef GD_K1
+    }
     GD_LAUNCH_CHECK("msda_bwd_samples");
     if (flags & GD_MSDA_DETERMINISTIC) {
       int bits = 1;
@@ -554,7 +569,7 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
   if (env_int("GD_MSDA_SORTED_K4", 0) != 1) {
     // K4 column sweep (+ chunk combine for the coarse levels)
     float* sw = reinterpret_cast<float*>(w + pl.o_sweep);
-    const int sblocks = (pl.W.tstart[4] + 3) / 4;
+    const int sblocks = (pl.W.ntasks + 3) / 4;
     const int lpu = dt == GD_BF16 ? 4 : 8;
     const int cblocks = (pl.W.cstart[4] + 256 / lpu - 1) / (256 / lpu);
 #define GD_SW(T, TO)                                                                                          \

@@ -178,7 +178,7 @@ def _tn(a, b, out):
     library GEMM below its token threshold."""
     nh, t, o = a.shape
     i = b.shape[-1]
-    if t >= wgrad.MIN_TOKENS and _lib.enabled("wgrad"):
+    if t >= wgrad.TN_MIN_TOKENS and _lib.enabled("wgrad"):
         s = int(_lib.lib().gd_wgrad_splits_batched(t, o, i, nh))
         ws = wgrad._workspace(o, i, s * nh, a.device)
         _lib.call("gd_wgrad_batched", _lib.dtype_code(a), a.data_ptr(), a.stride(1), a.stride(0), b.data_ptr(),

@@ -31,7 +31,12 @@ _lib.register("gd_wgrad_splits_batched", [_i, _i, _i, _i])
 _lib.register("gd_wgrad_batched", [_i, _p, _i64, _i64, _p, _i64, _i64, _i, _i, _i, _i, _i, _p, _i, _p, _i64, _p,
                                    _p])
 
-MIN_TOKENS = 4096
+# split-K weight gradient from 512 tokens up: the decoder's Linears (1 800
+# query tokens) and the text side (512) included -- measured 2x faster than
+# the library GEMM + fp32 bias sum there too (15-19 vs 28-34 us,
+# tools/wgrad_microbench.py); the long-K BiAttention products keep 4096
+MIN_TOKENS = 512
+TN_MIN_TOKENS = 4096
 ENABLED = True
 # Linears below the split-K kernel's token threshold (decoder: 1 800 query
 # tokens, text: 512): dW through the library's bf16 x bf16 -> fp32 GEMM
@@ -42,7 +47,7 @@ FP32_OUT_GEMM = os.environ.get("GDINO_FP32_WGRAD", "1") != "0"
 
 
 def eligible(x: torch.Tensor, out_features: int, dtype=None) -> bool:
-    """Route a Linear's weight gradient to the split-K kernel: GPU, T >= 4096
+    """Route a Linear's weight gradient to the split-K kernel: GPU, T >= MIN_TOKENS
     tokens, O and I multiples of 16 (bf16, the 128 x 128 transposed-read
     kernel) or of 64 (fp32); ``dtype``: the dtype the GEMM runs in (the
     autocast dtype), default x's.  Measured 2.4-6x faster than the library GEMM
@@ -116,7 +121,7 @@ def tn_eligible(a: torch.Tensor, b: torch.Tensor) -> bool:
     gran = 16 if a.dtype == torch.bfloat16 else 64
     return (_lib.enabled("wgrad") and _lib.on_device(a) and a.dtype == b.dtype
             and a.dtype in (torch.float32, torch.bfloat16) and a.shape[:-1] == b.shape[:-1]
-            and a.shape[-2] >= MIN_TOKENS and a.shape[-1] % gran == 0 and b.shape[-1] % gran == 0)
+            and a.shape[-2] >= TN_MIN_TOKENS and a.shape[-1] % gran == 0 and b.shape[-1] % gran == 0)
 
 
 def tn_matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -202,6 +202,15 @@ inline V update_dpp(V old, V src, int ctrl, int row_mask, int bank_mask, bool) {
   } else if (ctrl >= 0x121 && ctrl <= 0x12F) {  // row_ror:n
     const unsigned n = unsigned(ctrl) & 0xF;
     from = (lane & ~15u) | (((lane & 15u) + n) & 15u);
+  } else if ((ctrl >= 0x101 && ctrl <= 0x10F) || (ctrl >= 0x111 && ctrl <= 0x11F)) {
+    // row_shl:n / row_shr:n (bound_ctrl off): a lane whose source lies
+    // outside its 16-lane row keeps `old`
+    const unsigned n = unsigned(ctrl) & 0xF;
+    const int r = int(lane & 15u) + (ctrl <= 0x10F ? int(n) : -int(n));
+    const bool inside = r >= 0 && r <= 15;
+    from = inside ? (lane & ~15u) | unsigned(r) : lane;
+    const V got = xchg_from(src, wave_base() + from);
+    return inside ? got : old;
   } else {
     fprintf(stderr, "gd_emu: DPP control 0x%x not emulated\n", ctrl);
     abort();

@@ -139,6 +139,17 @@ def test_emulated_sorted_backward_matches_oracle(levels, n, lq, local, outliers,
     _check_sorted(inputs, levels, 1e-5)
 
 
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+def test_emulated_sorted_backward_level_by_level_per_sample_pass(vdtype, monkeypatch):
+    """GD_MSDA_SORTED_K1=2: the level-by-level per-sample pass (one level's
+    partials live at a time, its owned sample's record stored per level; the
+    A/B alternative to the default that holds all four levels)."""
+    monkeypatch.setenv("GD_MSDA_SORTED_K1", "2")
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=17, vdtype=vdtype, local=True, outlier_frac=0.05)
+    _check_sorted(inputs, MEDIUM, 1e-5)
+
+
 def test_emulated_sorted_backward_bf16_grad_value_and_determinism():
     """grad_value written directly in bf16 (the autograd dtype of a bf16
     value) equals the fp32 result rounded; the deterministic mode sorts each

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 T() { timeout -k 10 "$@"; }
 step() { echo "[$(date +%T)] $*"; }
 step parity
-T 900 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py tests/test_fullsize_gpu.py -x -q --timeout 300 --timeout-method thread -k "bi_att or biattn or fusion or block or cfg" > gpurun_out/q_parity.log 2>&1
+T 900 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py tests/test_fullsize_gpu.py -x -q --timeout 300 --timeout-method thread -k "bi_att or biattn or fusion or block or cfg or layer_norm or layernorm or twin or token_linear or linear_relu" > gpurun_out/q_parity.log 2>&1
 rc=$?; tail -2 gpurun_out/q_parity.log; [ $rc -ne 0 ] && exit $rc
 step microbench
 T 300 python3 tools/msda_microbench.py --bwd-variants --iters 20 > gpurun_out/q_bwd_variants.jsonl 2>&1 || exit $?
