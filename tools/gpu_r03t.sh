@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 T() { timeout -k 10 "$@"; }
 step() { echo "[$(date +%T)] $*"; }
 step parity
-T 600 python3 -u -m pytest tests/test_msda_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_parity.log 2>&1
+T 900 python3 -u -m pytest tests/test_msda_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_parity.log 2>&1
 rc=$?; tail -2 gpurun_out/t_parity.log; [ $rc -ne 0 ] && exit $rc
 step microbench
 T 300 python3 tools/msda_microbench.py --bwd-variants --iters 20 > gpurun_out/t_bwd_variants.jsonl 2>&1 || exit $?
