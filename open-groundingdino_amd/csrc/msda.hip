@@ -463,6 +463,7 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
     W.cstart[4] = int(items);
     if (tasks * N * M >= (int64_t(1) << 30) || items >= (int64_t(1) << 30)) return false;
     W.ntasks = int(tasks * N * M);
+    W.hp = (M % 2 == 0 && env_int("GD_MSDA_SORTED_HP", 2) == 2) ? 2 : 1;
     pl.o_sweep = o;
     o = align_up(o + sizeof(float) * size_t(pfl));
   }
@@ -546,15 +547,21 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
                            (const float*)loc, (const float*)attn, (const float*)grad_out, (float*)grad_loc,
                            (float*)grad_attn, cur, ids, pl.G, S, Lq, M, units);
     } else {
-#define GD_K1(T, P)                                                                                              \
-  hipLaunchKernelGGL((msda_bwd_samples<T, P>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,             \
+#define GD_K1(T, P, HP)                                                                                          \
+  hipLaunchKernelGGL((msda_bwd_samples<T, P, HP>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,         \
                      (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_loc, (float*)grad_attn, \
                      cur, ids, pl.G, S, Lq, M, units)
-    if (dt == GD_BF16) {
-      if (pipe) GD_K1(uint16_t, true); else GD_K1(uint16_t, false);
-    } else {
-      if (pipe) GD_K1(float, true); else GD_K1(float, false);
-    }
+      // heads in pairs (M even; GD_MSDA_SORTED_HP=1: one head per wave, A/B)
+      const bool hp = M % 2 == 0 && env_int("GD_MSDA_SORTED_HP", 2) == 2;
+      if (dt == GD_BF16) {
+        if (pipe) GD_K1(uint16_t, true, 1);
+        else if (hp) GD_K1(uint16_t, false, 2);
+        else GD_K1(uint16_t, false, 1);
+      } else {
+        if (pipe) GD_K1(float, true, 1);
+        else if (hp) GD_K1(float, false, 2);
+        else GD_K1(float, false, 1);
+      }
 #undef GD_K1
     }
     GD_LAUNCH_CHECK("msda_bwd_samples");

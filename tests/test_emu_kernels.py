@@ -150,6 +150,15 @@ def test_emulated_sorted_backward_level_by_level_per_sample_pass(vdtype, monkeyp
     _check_sorted(inputs, MEDIUM, 1e-5)
 
 
+def test_emulated_sorted_backward_one_head_per_wave(monkeypatch):
+    """GD_MSDA_SORTED_HP=1: per-sample pass and sweep with one head per wave
+    (the default pairs heads m, m + 1 for value / grad_out line reuse)."""
+    monkeypatch.setenv("GD_MSDA_SORTED_HP", "1")
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=19, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
+    _check_sorted(inputs, MEDIUM, 1e-5)
+
+
 def test_emulated_sorted_backward_bf16_grad_value_and_determinism():
     """grad_value written directly in bf16 (the autograd dtype of a bf16
     value) equals the fp32 result rounded; the deterministic mode sorts each

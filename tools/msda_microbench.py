@@ -193,6 +193,7 @@ BWD_VARIANTS = [
     ("sorted", {"GD_MSDA_BWD": "sorted"}),
     ("sorted cellsum", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K4": "1"}),
     ("sorted k1-level-by-level", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1": "2"}),
+    ("sorted one-head-per-wave", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_HP": "1"}),
     ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
     ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
     ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
@@ -216,7 +217,8 @@ def bwd_variants(iters):
         for name, env in reversed(BWD_VARIANTS):
             saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC", "GD_MSDA_SORTED_PROBE",
                                                     "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE",
-                                                    "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1")}
+                                                    "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1",
+                                                    "GD_MSDA_SORTED_HP")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
