@@ -579,10 +579,16 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
     const int sblocks = (pl.W.ntasks + 3) / 4;
     const int lpu = dt == GD_BF16 ? 4 : 8;
     const int cblocks = (pl.W.cstart[4] + 256 / lpu - 1) / (256 / lpu);
+    // GD_MSDA_SWEEP_PF=1: next row's first records loaded during this row's
+    // exchange (one dependent load less per row; 132 VGPRs)
+    const bool pf = env_int("GD_MSDA_SWEEP_PF", 0) == 1;
 #define GD_SW(T, TO)                                                                                          \
   do {                                                                                                        \
-    if (sblocks > 0)                                                                                          \
-      hipLaunchKernelGGL((msda_bwd_sweep<T, TO>), dim3(sblocks), dim3(256), 0, s, (const T*)grad_out,           \
+    if (sblocks > 0 && pf)                                                                                    \
+      hipLaunchKernelGGL((msda_bwd_sweep<T, TO, true>), dim3(sblocks), dim3(256), 0, s, (const T*)grad_out,     \
+                         (const int*)off, (const int4*)ids, (TO*)grad_value, sw, pl.G, pl.W, S, M);           \
+    else if (sblocks > 0)                                                                                     \
+      hipLaunchKernelGGL((msda_bwd_sweep<T, TO, false>), dim3(sblocks), dim3(256), 0, s, (const T*)grad_out,    \
                          (const int*)off, (const int4*)ids, (TO*)grad_value, sw, pl.G, pl.W, S, M);           \
     GD_LAUNCH_CHECK("msda_bwd_sweep");                                                                        \
     if (cblocks > 0)                                                                                          \

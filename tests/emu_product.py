@@ -21,13 +21,14 @@ def emulated_product(min_tokens=None):
         fn = getattr(emu, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
-    saved = (_lib._lib, _lib.on_device, _lib.stream_of, wgrad.MIN_TOKENS)
+    saved = (_lib._lib, _lib.on_device, _lib.stream_of, wgrad.MIN_TOKENS, wgrad.TN_MIN_TOKENS)
     _lib._lib = emu
     _lib.on_device = lambda t: True
     _lib.stream_of = lambda t: None
-    if min_tokens is not None:
+    if min_tokens is not None:  # the split-K thresholds (weight gradients, long-K products)
         wgrad.MIN_TOKENS = min_tokens
+        wgrad.TN_MIN_TOKENS = min_tokens
     try:
         yield
     finally:
-        _lib._lib, _lib.on_device, _lib.stream_of, wgrad.MIN_TOKENS = saved
+        _lib._lib, _lib.on_device, _lib.stream_of, wgrad.MIN_TOKENS, wgrad.TN_MIN_TOKENS = saved

@@ -150,6 +150,15 @@ def test_emulated_sorted_backward_level_by_level_per_sample_pass(vdtype, monkeyp
     _check_sorted(inputs, MEDIUM, 1e-5)
 
 
+def test_emulated_sorted_backward_sweep_record_prefetch(monkeypatch):
+    """GD_MSDA_SWEEP_PF=1: the sweep loads a row's first records during the
+    previous row's exchange."""
+    monkeypatch.setenv("GD_MSDA_SWEEP_PF", "1")
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=23, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
+    _check_sorted(inputs, MEDIUM, 1e-5)
+
+
 def test_emulated_sorted_backward_one_head_per_wave(monkeypatch):
     """GD_MSDA_SORTED_HP=1: per-sample pass and sweep with one head per wave
     (the default pairs heads m, m + 1 for value / grad_out line reuse)."""
@@ -374,7 +383,7 @@ import torch
 import test_emu_kernels as t
 S = sum(h * w for h, w in t.MEDIUM)
 """
-# three groups, run as concurrent processes (the ASan build is ~10x slower)
+# four groups, run as concurrent processes (the ASan build is ~10x slower)
 _ASAN_GROUPS = [
     r"""
 t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=3, local=True, outlier_frac=0.1), 1e-5)
@@ -382,12 +391,24 @@ t._check_bwd(t._levels_inputs(t.MEDIUM, 1, 37, seed=6), 1e-5)
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=8, local=True, outlier_frac=0.02), 1e-5,
              host_shapes=t.WIDE)
 import os
-for v in ("enc", "tiled"):
+for v in ("enc", "tiled"):  # the round-1/2 encoder kernels (A/B only since round 3)
     os.environ["GD_MSDA_BWD"] = v
     t._check_bwd(t._levels_inputs(t.MEDIUM, 2, S, seed=5, local=True, outlier_frac=0.1), 1e-5, host_shapes=t.MEDIUM)
-    t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=9, local=True, spread_px=6.0,
-                                  outlier_frac=0.02, vdtype=torch.bfloat16), 1e-5, host_shapes=t.WIDE)
 del os.environ["GD_MSDA_BWD"]
+""",
+    r"""
+# the sorted backward (the encoder default): both per-sample passes, both
+# grad_value kernels, the coarse-level chunks, the deterministic sort
+import os
+inp = t._levels_inputs(t.MEDIUM, 2, S, seed=21, vdtype=torch.bfloat16, local=True, outlier_frac=0.1)
+t._check_sorted(inp, t.MEDIUM, 1e-5)
+t._check_sorted(inp, t.MEDIUM, 1e-5, deterministic=True)
+os.environ["GD_MSDA_SORTED_K1"] = "2"
+os.environ["GD_MSDA_SORTED_K4"] = "1"
+t._check_sorted(t._levels_inputs(t.WIDE, 1, 23, seed=22, vdtype=torch.float32, local=False), t.WIDE, 1e-5)
+del os.environ["GD_MSDA_SORTED_K1"], os.environ["GD_MSDA_SORTED_K4"]
+t.test_emulated_sorted_backward_long_cell_segments(300)
+t.test_emulated_add_layernorm(41, 96, torch.float32, None)
 """,
     r"""
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)

@@ -176,3 +176,37 @@ def test_bi_attention_long_k_products_on_the_split_k_kernel():
     assert _rel(ov, rv) < 1e-5 and _rel(ol, rl) < 1e-5
     for a, r in zip(mine, ref):
         assert _rel(a.grad, r.grad) < 1e-5
+
+
+def test_bi_attention_token_major_core_on_the_emulated_kernels():
+    """biattn.BiAttnTokens (the model's path: joint projection outputs read
+    through strided per-head views, the scale on k, one gradient tensor per
+    joint output) with the softmax kernels and the split-K long-K products
+    emulated, fp32, against the reference restatement with gradients."""
+    from gdino_amd import biattn
+    from oracle.blocks import bi_attention_ref
+    g = torch.Generator().manual_seed(2)
+    b, h, s, t, hd = 2, 2, 300, 64, 64
+    e, scale = h * hd, hd ** -0.5
+    qvv = torch.randn(b, s, 2 * e, generator=g)
+    klv = torch.randn(b, t, 2 * e, generator=g)
+    pad_v = torch.zeros(b, s, dtype=torch.bool)
+    pad_v[1, 250:] = True
+    pad_l = torch.zeros(b, t, dtype=torch.bool)
+    pad_l[0, 40:] = True
+    gv, gl = torch.randn(b, s, e, generator=g), torch.randn(b, t, e, generator=g)
+    mine = [x.clone().requires_grad_(True) for x in (qvv, klv)]
+    with emu_product.emulated_product(min_tokens=64):
+        assert biattn.tokens_ok(*mine, h)
+        ov, ol = biattn.BiAttnTokens.apply(mine[0], mine[1], pad_v, pad_l, h, scale)
+        ((ov * gv).sum() + (ol * gl).sum()).backward()
+    ref = [x.double().requires_grad_(True) for x in (qvv, klv)]
+    hv = lambda x: x.unflatten(-1, (h, hd)).transpose(1, 2)  # noqa: E731
+    rv, rl = bi_attention_ref(hv(ref[0][..., :e]) * scale, hv(ref[1][..., :e]), hv(ref[0][..., e:]),
+                              hv(ref[1][..., e:]), pad_v, pad_l)
+    tok = lambda x: x.transpose(1, 2).reshape(x.shape[0], x.shape[2], e)  # noqa: E731
+    rv, rl = tok(rv), tok(rl)
+    ((rv * gv.double()).sum() + (rl * gl.double()).sum()).backward()
+    assert _rel(ov, rv) < 1e-5 and _rel(ol, rl) < 1e-5
+    for a, r in zip(mine, ref):
+        assert _rel(a.grad, r.grad) < 1e-5

@@ -194,6 +194,7 @@ BWD_VARIANTS = [
     ("sorted cellsum", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K4": "1"}),
     ("sorted k1-level-by-level", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1": "2"}),
     ("sorted one-head-per-wave", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_HP": "1"}),
+    ("sorted sweep-prefetch", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SWEEP_PF": "1"}),
     ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
     ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
     ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
@@ -203,22 +204,26 @@ BWD_VARIANTS = [
 ]
 
 
-def bwd_variants(iters):
+def bwd_variants(iters, only_geom=None, only_variant=None):
     """The backward as the model calls it (bf16 value, host level shapes,
     grad_value returned in bf16) under each kernel, encoder shape at the init
     geometry and a 2-px spread, and the decoder shape; checked against lane32."""
     S = sum(h * w for h, w in LEVELS)
     for geom in ("enc-init", "enc-spread2", "dec"):
+        if only_geom and geom != only_geom:
+            continue
         v, sh, ls, loc, attn, go = inputs(900 if geom == "dec" else S, torch.bfloat16)
         if geom == "enc-init":
             loc = init_geometry_loc(2)
         lq = loc.shape[1]
         ref = None
         for name, env in reversed(BWD_VARIANTS):
+            if only_variant and name != only_variant:
+                continue
             saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC", "GD_MSDA_SORTED_PROBE",
                                                     "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE",
                                                     "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1",
-                                                    "GD_MSDA_SORTED_HP")}
+                                                    "GD_MSDA_SORTED_HP", "GD_MSDA_SWEEP_PF")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
@@ -250,9 +255,11 @@ def main():
     ap.add_argument("--enc-probes", action="store_true")
     ap.add_argument("--enc-caps", action="store_true")
     ap.add_argument("--bwd-variants", action="store_true")
+    ap.add_argument("--geom", default=None, help="with --bwd-variants: enc-init | enc-spread2 | dec only")
+    ap.add_argument("--variant", default=None, help="with --bwd-variants: one variant name only")
     args = ap.parse_args()
     if args.bwd_variants:
-        bwd_variants(args.iters)
+        bwd_variants(args.iters, args.geom, args.variant)
         return
     if args.fwd_variants:
         fwd_variants(args.iters)
