@@ -364,7 +364,7 @@ struct SortedPlan {
   SweepGeo W;
   int ncells = 0, nsamples = 0, nb = 0, k1_blocks = 0;
   size_t o_sweep = 0;  // K4 sweep: partial rows of the chunked levels
-  size_t o_cnt = 0, o_off = 0, o_cur = 0, o_bsum = 0, o_ids = 0, o_part = 0, o_scr = 0, bytes = 0;
+  size_t o_cnt = 0, o_off = 0, o_cur = 0, o_bsum = 0, o_ids = 0, o_part = 0, o_scr = 0, o_stat = 0, bytes = 0;
 };
 
 inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -420,7 +420,7 @@ bool plan_sorted(gd_dtype dt, int N, int S, int M, int D, int L, int Lq, int P, 
   if (pl.nb > 256 * kScanPer) return false;
   pl.k1_blocks = int((units + upb - 1) / upb);
   size_t o = 0;
-  pl.o_cnt = o; o = align_up(o + sizeof(int) * size_t(ncells));        // cell counts
+  pl.o_cnt = o; o = align_up(o + sizeof(int) * size_t(ncells + 2));    // cell counts + 2 run statistics
   pl.o_off = o; o = align_up(o + sizeof(int) * size_t(ncells + 1));    // segment offsets
   pl.o_bsum = o; o = align_up(o + sizeof(int) * size_t(pl.nb));
   pl.o_cur = o; o = align_up(o + sizeof(int) * size_t(ncells));        // segment cursors (K1)
@@ -518,10 +518,19 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
   int4* scr = reinterpret_cast<int4*>(w + pl.o_scr);
   float* part = reinterpret_cast<float*>(w + pl.o_part);
   const int units = pl.nsamples / 16;
-  GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells), s));
+  GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells + 2), s));
+  int* stat = cnt + pl.ncells;  // coarse runs / coarse samples of the first count blocks
   if (units > 0) {
-    hipLaunchKernelGGL(msda_bwd_count, dim3((units + 63) / 64), dim3(256), 0, s, (const float*)loc, cnt, pl.G, Lq, M,
-                       units);
+    // coarse-level counts through a per-workgroup LDS histogram when both
+    // (n, m) slots of it fit (GD_MSDA_COUNT_PRIV=0: all global atomics, A/B)
+    const int c23 = (pl.G.H[2] + 1) * (pl.G.W[2] + 1) + (pl.G.H[3] + 1) * (pl.G.W[3] + 1);
+    const bool priv = Lq >= 64 && 2 * c23 <= kCountBins && env_int("GD_MSDA_COUNT_PRIV", 1) != 0;
+    if (priv)
+      hipLaunchKernelGGL(msda_bwd_count<true>, dim3((units + 63) / 64), dim3(256), 0, s, (const float*)loc, cnt, stat,
+                         pl.G, Lq, M, units);
+    else
+      hipLaunchKernelGGL(msda_bwd_count<false>, dim3((units + 63) / 64), dim3(256), 0, s, (const float*)loc, cnt,
+                         stat, pl.G, Lq, M, units);
     GD_LAUNCH_CHECK("msda_bwd_count");
   }
   hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);
@@ -550,9 +559,17 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
 #define GD_K1(T, P, HP)                                                                                          \
   hipLaunchKernelGGL((msda_bwd_samples<T, P, HP>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,         \
                      (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_loc, (float*)grad_attn, \
-                     cur, ids, pl.G, S, Lq, M, units)
+                     cur, ids, pl.G, S, Lq, M, units, kpriv ? (const int*)stat : nullptr)
       // heads in pairs (M even; GD_MSDA_SORTED_HP=1: one head per wave, A/B)
       const bool hp = M % 2 == 0 && env_int("GD_MSDA_SORTED_HP", 2) == 2;
+      // coarse-level slots through the LDS histogram (2 or 4 (n, m) slots)
+      const int kc23 = (pl.G.H[2] + 1) * (pl.G.W[2] + 1) + (pl.G.H[3] + 1) * (pl.G.W[3] + 1);
+      // (the per-sample pass decides on the device from the count pass's run
+      // statistics; GD_MSDA_COUNT_PRIV=0 disables both histograms, =2
+      // forces K1's regardless of run length -- A/B)
+      const int kenv = env_int("GD_MSDA_COUNT_PRIV", 1);
+      const int kpriv = (Lq >= 64 && (hp && !pipe ? 4 : 2) * kc23 <= kCountBins && kenv != 0) ? 1 : 0;
+      if (kpriv && kenv == 2) GD_HIP_CHECK(hipMemsetAsync(stat, 0x10, sizeof(int), s));  // runs >> samples
       if (dt == GD_BF16) {
         if (pipe) GD_K1(uint16_t, true, 1);
         else if (hp) GD_K1(uint16_t, false, 2);

@@ -150,6 +150,19 @@ def test_emulated_sorted_backward_level_by_level_per_sample_pass(vdtype, monkeyp
     _check_sorted(inputs, MEDIUM, 1e-5)
 
 
+@pytest.mark.parametrize("priv", ["0", "2"])
+def test_emulated_sorted_backward_lds_histograms(priv, monkeypatch):
+    """GD_MSDA_COUNT_PRIV=0: every count / slot a global atomic; =2: the
+    per-sample pass reserves the coarse levels' slots through its LDS
+    histogram whatever the run statistics say (the default decides on the
+    device), with both (n, m) and head-pair slots in play (batch of 2)."""
+    monkeypatch.setenv("GD_MSDA_COUNT_PRIV", priv)
+    S = sum(h * w for h, w in MEDIUM)
+    for vd in (torch.float32, torch.bfloat16):
+        inputs = _levels_inputs(MEDIUM, 2, S, seed=29, vdtype=vd, local=True, outlier_frac=0.1)
+        _check_sorted(inputs, MEDIUM, 1e-5)
+
+
 def test_emulated_sorted_backward_sweep_record_prefetch(monkeypatch):
     """GD_MSDA_SWEEP_PF=1: the sweep loads a row's first records during the
     previous row's exchange."""

@@ -195,6 +195,8 @@ BWD_VARIANTS = [
     ("sorted k1-level-by-level", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1": "2"}),
     ("sorted one-head-per-wave", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_HP": "1"}),
     ("sorted sweep-prefetch", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SWEEP_PF": "1"}),
+    ("sorted no-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "0"}),
+    ("sorted forced-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "2"}),
     ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
     ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
     ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
@@ -223,7 +225,8 @@ def bwd_variants(iters, only_geom=None, only_variant=None):
             saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC", "GD_MSDA_SORTED_PROBE",
                                                     "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE",
                                                     "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1",
-                                                    "GD_MSDA_SORTED_HP", "GD_MSDA_SWEEP_PF")}
+                                                    "GD_MSDA_SORTED_HP", "GD_MSDA_SWEEP_PF",
+                                                    "GD_MSDA_COUNT_PRIV")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
