@@ -556,8 +556,8 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
                            (const float*)loc, (const float*)attn, (const float*)grad_out, (float*)grad_loc,
                            (float*)grad_attn, cur, ids, pl.G, S, Lq, M, units);
     } else {
-#define GD_K1(T, P, HP)                                                                                          \
-  hipLaunchKernelGGL((msda_bwd_samples<T, P, HP>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,         \
+#define GD_K1(T, P, HP, LL)                                                                                      \
+  hipLaunchKernelGGL((msda_bwd_samples<T, P, HP, LL>), dim3(pl.k1_blocks), dim3(256), 0, s, (const T*)value,     \
                      (const float*)loc, (const float*)attn, (const T*)grad_out, (float*)grad_loc, (float*)grad_attn, \
                      cur, ids, pl.G, S, Lq, M, units, kpriv ? (const int*)stat : nullptr)
       // heads in pairs (M even; GD_MSDA_SORTED_HP=1: one head per wave, A/B)
@@ -570,14 +570,21 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       const int kenv = env_int("GD_MSDA_COUNT_PRIV", 1);
       const int kpriv = (Lq >= 64 && (hp && !pipe ? 4 : 2) * kc23 <= kCountBins && kenv != 0) ? 1 : 0;
       if (kpriv && kenv == 2) GD_HIP_CHECK(hipMemsetAsync(stat, 0x10, sizeof(int), s));  // runs >> samples
+      // locations loaded level by level (default; 146 instead of 192 VGPRs:
+      // 3 waves per SIMD): 345 -> 315 us at the init geometry, 510 -> 475 us
+      // on a 2-px spread (profiles/r03g); GD_MSDA_SORTED_LL=0: all 48
+      // location / weight floats held from the start
+      const bool ll = env_int("GD_MSDA_SORTED_LL", 1) == 1;
       if (dt == GD_BF16) {
-        if (pipe) GD_K1(uint16_t, true, 1);
-        else if (hp) GD_K1(uint16_t, false, 2);
-        else GD_K1(uint16_t, false, 1);
+        if (pipe) GD_K1(uint16_t, true, 1, false);
+        else if (hp && ll) GD_K1(uint16_t, false, 2, true);
+        else if (hp) GD_K1(uint16_t, false, 2, false);
+        else GD_K1(uint16_t, false, 1, false);
       } else {
-        if (pipe) GD_K1(float, true, 1);
-        else if (hp) GD_K1(float, false, 2);
-        else GD_K1(float, false, 1);
+        if (pipe) GD_K1(float, true, 1, false);
+        else if (hp && ll) GD_K1(float, false, 2, true);
+        else if (hp) GD_K1(float, false, 2, false);
+        else GD_K1(float, false, 1, false);
       }
 #undef GD_K1
     }

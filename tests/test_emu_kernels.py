@@ -172,6 +172,17 @@ def test_emulated_sorted_backward_sweep_record_prefetch(monkeypatch):
     _check_sorted(inputs, MEDIUM, 1e-5)
 
 
+@pytest.mark.parametrize("vdtype", [torch.float32, torch.bfloat16])
+def test_emulated_sorted_backward_locations_held(vdtype, monkeypatch):
+    """GD_MSDA_SORTED_LL=0: the per-sample pass holds all 48 location /
+    weight floats from the start (the default loads them level by level and
+    reloads the owned samples'), head pairs, batch of 2."""
+    monkeypatch.setenv("GD_MSDA_SORTED_LL", "0")
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=23, vdtype=vdtype, local=True, outlier_frac=0.05)
+    _check_sorted(inputs, MEDIUM, 1e-5)
+
+
 def test_emulated_sorted_backward_one_head_per_wave(monkeypatch):
     """GD_MSDA_SORTED_HP=1: per-sample pass and sweep with one head per wave
     (the default pairs heads m, m + 1 for value / grad_out line reuse)."""

@@ -400,6 +400,27 @@ def test_sorted_backward_deterministic_mode_is_bitwise_reproducible(lq, monkeypa
     assert torch.equal(fast[1], runs[0][1]) and torch.equal(fast[2], runs[0][2])
 
 
+@pytest.mark.parametrize("geometry", ["init", "spread"])
+def test_sorted_level_loaded_locations_are_bitwise_the_default(geometry, monkeypatch):
+    """The default per-sample pass (locations loaded level by level,
+    reloaded for the owned samples) does the same arithmetic as
+    GD_MSDA_SORTED_LL=0 (all held from the start): in deterministic mode all
+    three gradients are bitwise equal."""
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "1")
+    value, shapes, lsi, loc, attn, grad_out = _encoder_inputs(LEVELS_800, 2, seed=43, vdtype=torch.bfloat16,
+                                                              outlier_frac=0.02)
+    if geometry == "init":
+        loc = _init_geometry_loc(LEVELS_800, 2)
+    inputs = [t.to(DEV) for t in (value, shapes, lsi, loc, attn, grad_out)]
+    runs = []
+    for ll in ("0", "1"):
+        monkeypatch.setenv("GD_MSDA_SORTED_LL", ll)
+        runs.append(_msda().ms_deform_attn_backward(*inputs, 64, host_shapes=LEVELS_800))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 def test_sorted_backward_bf16_grad_value_is_the_rounded_fp32_sum(monkeypatch):
     """grad_value in bf16 straight from the kernel equals the kernel's fp32
     result rounded to bf16 (same sums, deterministic mode)."""

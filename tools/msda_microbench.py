@@ -194,6 +194,7 @@ BWD_VARIANTS = [
     ("sorted cellsum", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K4": "1"}),
     ("sorted k1-level-by-level", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1": "2"}),
     ("sorted one-head-per-wave", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_HP": "1"}),
+    ("sorted locations-held", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_LL": "0"}),
     ("sorted sweep-prefetch", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SWEEP_PF": "1"}),
     ("sorted no-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "0"}),
     ("sorted forced-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "2"}),
@@ -226,7 +227,7 @@ def bwd_variants(iters, only_geom=None, only_variant=None):
                                                     "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE",
                                                     "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1",
                                                     "GD_MSDA_SORTED_HP", "GD_MSDA_SWEEP_PF",
-                                                    "GD_MSDA_COUNT_PRIV")}
+                                                    "GD_MSDA_COUNT_PRIV", "GD_MSDA_SORTED_LL")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
