@@ -31,6 +31,18 @@ per step.
 The cache is bypassed while a HIP graph is being captured: a graph must
 contain the cast, or its replays would read a stale copy after the optimizer
 step.
+
+Step shadows (``refresh_shadows``, GDINO_CAST_SHADOWS=0 to disable): at the
+start of every training forward (GroundingDINO.forward_core, so also inside
+the captured forward graph) ONE multi-tensor copy kernel casts every
+trainable fp32 parameter into a persistent bf16 shadow, and cached_cast hands
+out the shadow (through _ShadowCast, whose backward is ToCopyBackward's
+grad.to(fp32)) while it is current: same generation, same parameter version.
+A captured step thus carries one cast launch instead of one per Linear call
+(several hundred graph nodes, the checkpoint recomputes included).  Frozen
+parameters (the BERT) keep their one eager cast, also under capture (a
+frozen weight loaded after capture needs a re-capture, as any graph input
+whose storage is replaced does).
 """
 from __future__ import annotations
 
@@ -81,20 +93,98 @@ def _capturing(p: torch.Tensor) -> bool:
     return p.is_cuda and torch.cuda.is_current_stream_capturing()
 
 
+SHADOWS = os.environ.get("GDINO_CAST_SHADOWS", "1") != "0"
+_shadow: dict = {}       # id(p) -> [weakref(p), bf16 shadow, p._version at the refresh]
+_shadow_state = None     # (generation, dtype) of the last refresh
+
+
+class _ShadowCast(torch.autograd.Function):
+    """p -> its refreshed low-precision shadow; backward = ToCopyBackward."""
+
+    @staticmethod
+    def forward(ctx, p, shadow):
+        ctx.dtype = p.dtype
+        return shadow.detach()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dtype), None
+
+
+def _shadow_params(model: nn.Module):
+    ps = getattr(model, "_gd_shadow_params", None)
+    if ps is None:
+        seen, ps = set(), []
+        for q in model.parameters():
+            if q.requires_grad and q.dtype == torch.float32 and id(q) not in seen:
+                seen.add(id(q))
+                ps.append(q)
+        model._gd_shadow_params = ps
+    return ps
+
+
+def refresh_shadows(model: nn.Module, x: torch.Tensor) -> None:
+    """Cast every trainable fp32 parameter of ``model`` into its persistent
+    shadow in one multi-tensor copy, when a training forward under bf16
+    autocast is about to run (x: any input on the model's device)."""
+    global _shadow_state
+    dt = autocast_dtype(x) if SHADOWS else None
+    if dt is None or not torch.is_grad_enabled() or not model.training:
+        return
+    ps = _shadow_params(model)
+    if not ps or any(q.device != x.device for q in ps):
+        return
+    if _shadow_state == (_generation, dt) and not _capturing(x) and all(
+            _current_shadow(q, dt) is not None for q in ps):
+        return  # already this step's weights (a second forward before the optimizer step)
+    dsts, srcs = [], []
+    for q in ps:
+        e = _shadow.get(id(q))
+        if e is None or e[0]() is not q or e[1].shape != q.shape or e[1].dtype != dt:
+            e = [weakref.ref(q), torch.empty(q.shape, dtype=dt, device=q.device), None]
+            _shadow[id(q)] = e
+        e[2] = q._version
+        dsts.append(e[1])
+        srcs.append(q.detach())
+    with torch.no_grad():
+        torch._foreach_copy_(dsts, srcs)
+    _shadow_state = (_generation, dt)
+
+
+def _current_shadow(p: torch.Tensor, dtype: torch.dtype):
+    if _shadow_state != (_generation, dtype):
+        return None
+    e = _shadow.get(id(p))
+    if e is None or e[0]() is not p or e[2] != p._version:
+        return None
+    return e[1]
+
+
+def _from_shadow(p, s, grad):
+    return _ShadowCast.apply(p, s) if grad else s
+
+
 def cached_cast(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """Callers only use this when ENABLED (otherwise they hand the fp32
     parameter to autocast, whose own per-region cache then applies)."""
     if p.dtype == dtype:
         return p
     grad = torch.is_grad_enabled() and p.requires_grad
-    if _capturing(p):
-        return p.to(dtype)
     key = id(p)
     ver = (p._version, _gen(p.requires_grad))
+    sh = _current_shadow(p, dtype) if p.requires_grad else None
+    if _capturing(p):
+        if sh is not None:
+            return _from_shadow(p, sh, grad)
+        ent = _cache.get(key)
+        if not p.requires_grad and ent is not None and ent[0]() is p and ent[1] == ver and ent[2] == dtype \
+                and ent[3] == grad:
+            return ent[4]  # frozen: the eager copy made before capture
+        return p.to(dtype)
     ent = _cache.get(key)
     if ent is not None and ent[0]() is p and ent[1] == ver and ent[2] == dtype and ent[3] == grad:
         return ent[4]
-    t = p.to(dtype)
+    t = _from_shadow(p, sh, grad) if sh is not None else p.to(dtype)
     _cache[key] = (weakref.ref(p), ver, dtype, grad, t)
     if len(_cache) > 8192:  # drop entries of freed parameters
         for k in [k for k, v in _cache.items() if v[0]() is None]:
@@ -103,7 +193,10 @@ def cached_cast(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 
 def clear() -> None:
+    global _shadow_state
     _cache.clear()
+    _shadow.clear()
+    _shadow_state = None
 
 
 def _token_linear_ok(x, params, out_features, dt):
@@ -181,16 +274,23 @@ def _cached_cat(params, dtype):
     """bf16 concatenation (dim 0) of several parameters, cached like
     cached_cast; gradients reach each parameter through the cat's split."""
     ps = tuple(params)
-    if _capturing(ps[0]):
-        return torch.cat(ps).to(dtype)
+    shs = [_current_shadow(p, dtype) if p.requires_grad else None for p in ps]
     grad = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
+    if all(sh is not None for sh in shs):
+        def make():  # one bf16 cat of the step's shadows (no fp32 cat + cast)
+            return torch.cat([_from_shadow(p, sh, torch.is_grad_enabled()) for p, sh in zip(ps, shs)])
+    else:
+        def make():
+            return torch.cat(ps).to(dtype)  # = cat of the casts, one cast kernel (and one in backward)
+    if _capturing(ps[0]):
+        return make()
     key = ("cat",) + tuple(id(p) for p in ps)
     vers = tuple(p._version for p in ps) + (_gen(any(p.requires_grad for p in ps)),)
     ent = _cache.get(key)
     if ent is not None and all(r() is p for r, p in zip(ent[0], ps)) and ent[1] == vers and ent[2] == dtype \
             and ent[3] == grad:
         return ent[4]
-    t = torch.cat(ps).to(dtype)  # = cat of the casts, one cast kernel (and one in backward)
+    t = make()
     _cache[key] = (tuple(weakref.ref(p) for p in ps), vers, dtype, grad, t)
     return t
 

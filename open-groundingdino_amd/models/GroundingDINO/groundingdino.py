@@ -192,6 +192,7 @@ class GroundingDINO(nn.Module):
         captures into one HIP graph for forward and one for backward.
         -> (outputs_class [L,B,Q,256], outputs_coord [L,B,Q,4], text_mask [B,256],
             interm_class, interm_coord, init_box_proposal)"""
+        castcache.refresh_shadows(self, images)  # this step's bf16 weights, one launch
         text_dict = self.encode_text(input_ids, token_type_ids, text_token_mask, self_masks, position_ids)
         samples = NestedTensor(images, image_mask)
         features, poss = self.backbone(samples)

@@ -174,9 +174,10 @@ def test_cast_cache_is_bit_identical_under_autocast(built):
     model.train()
     assert any(isinstance(m, castcache.CachedCastLinear) for m in model.modules())
 
-    def run(enabled, fuse=False, amp=True):
+    def run(enabled, fuse=False, amp=True, shadows=True):
         castcache.ENABLED = enabled
         castcache.FUSE_SHARED_INPUT = fuse
+        castcache.SHADOWS = shadows
         castcache.clear()
         torch.manual_seed(7)
         for p in model.parameters():
@@ -187,21 +188,26 @@ def test_cast_cache_is_bit_identical_under_autocast(built):
                 ld = criterion(out, targets, cats, caps)
                 loss = sum(ld[k] * criterion.weight_dict[k] for k in ld if k in criterion.weight_dict)
             loss.backward()
+        # the step-shadow path (one multi-tensor cast per step) was taken
+        assert (len(castcache._shadow) > 100) == (enabled and amp and shadows)
         return loss.detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
 
     try:
         l0, g0 = run(False)
         l1, g1 = run(True)
+        ls, gs = run(True, shadows=False)
         l2, g2 = run(True, fuse=True)
         lf, gf = run(True, amp=False)
     finally:
         castcache.ENABLED = True
         castcache.FUSE_SHARED_INPUT = True
+        castcache.SHADOWS = True
         castcache.clear()
-    assert torch.equal(l0, l1)
-    assert g0.keys() == g1.keys() == g2.keys() and len(g0) > 100
+    assert torch.equal(l0, l1) and torch.equal(l0, ls)
+    assert g0.keys() == g1.keys() == g2.keys() == gs.keys() and len(g0) > 100
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+        assert torch.equal(g0[n], gs[n]), n
     # shared-input projections as one GEMM: same math (pinned at 1e-9 in fp64
     # by test_blocks_golden), GEMM blocking may round differently in bf16 ->
     # must stay within the bf16-vs-fp32 noise of the unfused path

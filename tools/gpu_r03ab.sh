@@ -19,6 +19,14 @@ for l in open('gpurun_out/ab_bench.log'):
     if l.startswith('{'):
         d=json.loads(l); print('bench', round(d['value'],2), 'img/s', round(d['ms_per_step'],1), 'ms', d['step_ms'], d['roofline'])
 "
+step bench-no-shadows
+GDINO_CAST_SHADOWS=0 T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/ab_bench_noshadow.log 2>&1 || exit $?
+python3 -c "
+import json
+for l in open('gpurun_out/ab_bench_noshadow.log'):
+    if l.startswith('{'):
+        d=json.loads(l); print('bench no-shadows', round(d['value'],2), 'img/s', round(d['ms_per_step'],1), 'ms', d['step_ms'])
+"
 step trace
 cd /tmp && T 500 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ab_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/ab_prof.log 2>&1 || exit $?
 cd $GRAFT_REPO_ROOT
