@@ -50,12 +50,15 @@ def parse(argv=None):
     ap.add_argument("--width", type=int, default=1333)
     ap.add_argument("--backbone", default="swin_T_224_1k")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--bucket-mb", type=float, default=25,
+                    help="gradient all-reduce bucket size (MB; the first bucket is 1 MB so the first collective "
+                         "starts early in the backward)")
     ap.add_argument("--forward-only", action="store_true",
                     help="BASELINE config 2: eval-mode forward (no autograd) instead of the train step")
     ap.add_argument("--graphs", dest="graphs", action="store_true", default=None,
-                    help="replay forward_core (fwd+bwd) as HIP graphs (default for the train step on the GPU; "
-                         "DESIGN.md section 7)")
+                    help="replay the whole train step (forward, device Hungarian matching + loss, backward with "
+                         "the overlapped gradient all-reduce, clip, AdamW) as ONE HIP graph (default for the train "
+                         "step on the GPU; DESIGN.md section 7)")
     ap.add_argument("--no-graphs", dest="graphs", action="store_false", help="eager train step")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
@@ -299,10 +302,11 @@ def main(argv=None, device_type="cuda", child_script=None):
     grad_sync = None
     if world > 1 and not a.forward_only:
         if use_graphs:
-            # DDP's bucket hooks cannot fire inside a graph replay: the same
-            # averaged gradients by a bucketed RCCL all-reduce after backward
-            from gdino_amd.train import GradAllReduce
-            grad_sync = GradAllReduce(model.parameters(), a.bucket_mb)
+            # DDP's reducer cannot follow graph replays: BucketedGradSync does
+            # the same bucketed, backward-overlapped all-reduce from
+            # post-accumulate hooks, captured into the step graph
+            from gdino_amd.train import BucketedGradSync
+            grad_sync = BucketedGradSync(model.parameters(), a.bucket_mb)
         else:
             # reference main.py:258-261 (DDP + static graph); buckets sized for
             # xGMI rings (fewer, larger all-reduces), launched as backward
@@ -320,23 +324,28 @@ def main(argv=None, device_type="cuda", child_script=None):
             return train_step(model, criterion, optimizer, samples, targets, captions, cats, grad_sync=grad_sync)
 
     graph_note = None
+    eager_step = step
+    step_graph = None
     if use_graphs:
         # GEMM library inside the captured region (GDINO_GRAPH_BLAS: "hipblaslt"
         # or "cublas" = rocBLAS on ROCm)
         blas = os.environ.get("GDINO_GRAPH_BLAS")
         if blas:
             torch.backends.cuda.preferred_blas_library(blas)
-        from gdino_amd import graphs
+        from gdino_amd.stepgraph import TrainStepGraph
+        step_graph = TrainStepGraph(model, criterion, optimizer, grad_sync=grad_sync)
         try:
-            text, _ = core.prepare_text(captions, device)
-            graphs.capture(core, (samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
-                                  text["text_token_mask"], text["self_masks"], text["position_ids"]))
+            step_graph(samples, targets, captions, cats)  # capture (+ its eager warm-up steps) and one replay
             sync()
         except Exception as e:  # capture refused: measure the eager step instead
-            graphs.release(core)
+            step_graph.release()
+            step_graph = None
             use_graphs = False
             graph_note = f"graph capture failed, eager step measured: {repr(e)[:200]}"
             print(f"warning: {graph_note}", file=sys.stderr, flush=True)
+        else:
+            def step():
+                return step_graph(samples, targets, captions, cats)
 
     for _ in range(a.warmup):
         step()
@@ -390,12 +399,10 @@ def main(argv=None, device_type="cuda", child_script=None):
     hip_calls = None
     if on_gpu and world == 1:
         if use_graphs:  # the extra step runs eagerly: every C-ABI call is a Python call
-            from gdino_amd import graphs
-            graphs.release(core)
             msda.timer = msda.LaunchTimer()
         _lib.call_timer = _lib.CallTimer()
         try:
-            step()
+            eager_step()
             hip_calls = _lib.call_timer.summary()
             if use_graphs:
                 kern = msda.timer.summary()
@@ -457,8 +464,13 @@ def main(argv=None, device_type="cuda", child_script=None):
             "kernels": kernels,
             "hip_entry_points_one_step": hip_calls,
             "options": {"hip_graphs": bool(use_graphs), "graph_note": graph_note, "tunableop": a.tunableop,
-                        "grad_sync": ("bucketed all-reduce after the graphed backward" if grad_sync is not None
-                                      else ("DDP" if world > 1 and not a.forward_only else None)),
+                        "step_graph": ("whole train step (forward, device Hungarian matching + loss, backward, "
+                                       "all-reduce, clip, AdamW) as one HIP graph" if use_graphs else None),
+                        "grad_sync": (f"bucketed RCCL all-reduce overlapped with the backward (post-accumulate "
+                                      f"hooks, gradients as bucket views, captured in the step graph), buckets "
+                                      f"{[round(x, 1) for x in grad_sync.bucket_sizes_mb()]} MB"
+                                      if grad_sync is not None else
+                                      ("DDP (overlapped, eager step)" if world > 1 and not a.forward_only else None)),
                         # HIP kernel families on this run (GDINO_DISABLE turns them off for A/B)
                         "hip_families": ["msda", "biattn"] + [f for f in ("wattn", "attn", "contrastive", "prologue",
                                                                          "wgrad", "addln") if _lib.enabled(f)],

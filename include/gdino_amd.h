@@ -71,6 +71,12 @@
  *                        models/GroundingDINO/utils.py:242-273, and the
  *                        two-stage score enc_outputs_class_unselected.max(-1)
  *                        models/GroundingDINO/transformer.py:292-296
+ *   gd_linear_sum_assignment
+ *                     <- HungarianMatcher.forward's C.cpu() + per-image
+ *                        scipy.optimize.linear_sum_assignment
+ *                        models/GroundingDINO/matcher.py:104-110 (scipy 1.15
+ *                        rectangular_lsap: same algorithm, operation order and
+ *                        tie-breaking, on the device)
  */
 #ifndef GDINO_AMD_H
 #define GDINO_AMD_H
@@ -385,6 +391,25 @@ gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_
                                     const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,
                                     float* grad_weight, float* grad_bias, void* workspace,
                                     gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Hungarian matching (matcher.py:104-110)                                   */
+/* ------------------------------------------------------------------------ */
+/*
+ * cost    [problems][Q][K] F32 (problem p at cost + p * problem_stride,
+ *         row-major [Q, K]); problem p uses its first n_p = sizes[p] columns
+ *         (the targets; device memory, int32).
+ * Solves linear_sum_assignment(cost[p][:, :n_p]) exactly as scipy 1.15 does
+ * (float64, same tie-breaking) and writes its min(Q, n_p) pairs in ascending
+ * row (query) order: out_row[p][r] = query, out_col[p][r] = target, r <
+ * min(Q, n_p); the remaining K - min(Q, n_p) slots get -1.  status[p] (or
+ * NULL): 0, or 1 when scipy would raise (infeasible: +inf costs), in which
+ * case the pairs are the reference's fallback (argmin query per target,
+ * matcher.py:111-119).  Limits: max(Q, K) <= 2048, min(Q, K) or Q <= 1024.
+ */
+gd_status gd_linear_sum_assignment(const float* cost, int problems, int Q, int K, int64_t problem_stride,
+                                   const int* sizes, int64_t* out_row, int64_t* out_col, int* status,
+                                   gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime                                                                   */

@@ -171,6 +171,18 @@ def _hv(x2, nh):
     return x2.unflatten(-1, (nh, x2.shape[-1] // nh)).transpose(0, 1)
 
 
+def _tn_ok(a, b, o, i) -> bool:
+    """What gd_wgrad_batched accepts: o and i multiples of 16 (bf16) / 64
+    (fp32), unit channel stride, 16-B aligned rows and bases.  o is the text
+    length T when a is P_l / P_v / dS: captions pad to the longest in the
+    batch (groundingdino.py:56), so T is often not a multiple of 16."""
+    gran = 16 if a.dtype == torch.bfloat16 else 64
+    align = 16 // a.element_size()
+    return (a.dtype == b.dtype and a.dtype in (torch.float32, torch.bfloat16) and o % gran == 0 and i % gran == 0
+            and all(x.stride(-1) == 1 and x.stride(1) % align == 0 and x.stride(0) % align == 0
+                    and x.data_ptr() % 16 == 0 for x in (a, b)))
+
+
 def _tn(a, b, out):
     """out[h] = a[h]^T b[h] for [nh, L, o] / [nh, L, i] views contracting
     over the L image tokens (the long-K products): the split-K kernel of
@@ -178,7 +190,7 @@ def _tn(a, b, out):
     library GEMM below its token threshold."""
     nh, t, o = a.shape
     i = b.shape[-1]
-    if t >= wgrad.TN_MIN_TOKENS and _lib.enabled("wgrad"):
+    if t >= wgrad.TN_MIN_TOKENS and _lib.enabled("wgrad") and _tn_ok(a, b, o, i):
         s = int(_lib.lib().gd_wgrad_splits_batched(t, o, i, nh))
         ws = wgrad._workspace(o, i, s * nh, a.device)
         _lib.call("gd_wgrad_batched", _lib.dtype_code(a), a.data_ptr(), a.stride(1), a.stride(0), b.data_ptr(),

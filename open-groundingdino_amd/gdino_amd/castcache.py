@@ -112,15 +112,22 @@ class _ShadowCast(torch.autograd.Function):
 
 
 def _shadow_params(model: nn.Module):
-    ps = getattr(model, "_gd_shadow_params", None)
-    if ps is None:
+    """The trainable fp32 parameters, rebuilt whenever the parameter set or
+    a requires_grad flag changes (a later freeze / unfreeze, a
+    load_state_dict(assign=True), a re-wrap): a stale list would keep casting
+    frozen weights, or silently leave new ones on one cast per use."""
+    params = list(model.parameters())
+    sig = tuple((id(q), q.requires_grad, q.dtype) for q in params)
+    cached = getattr(model, "_gd_shadow_params", None)
+    if cached is None or cached[0] != sig:
         seen, ps = set(), []
-        for q in model.parameters():
+        for q in params:
             if q.requires_grad and q.dtype == torch.float32 and id(q) not in seen:
                 seen.add(id(q))
                 ps.append(q)
-        model._gd_shadow_params = ps
-    return ps
+        cached = (sig, ps)
+        model._gd_shadow_params = cached
+    return cached[1]
 
 
 def refresh_shadows(model: nn.Module, x: torch.Tensor) -> None:

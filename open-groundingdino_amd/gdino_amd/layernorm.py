@@ -24,12 +24,12 @@ _lib.register("gd_add_layernorm_forward", [_i, _p, _i, _p, _p, _p, _i64, _i, _f,
 _lib.register("gd_add_layernorm_forward2", [_i, _p, _i, _p, _p, _p, _i64, _i, _f, _p, _p, _p, _p, _p])
 
 
-def _bf16_twin_wanted(x) -> bool:
+def _bf16_twin_wanted(x, wanted: bool = True) -> bool:
     """Under bf16 autocast the fp32 LayerNorm output is cast again by every
     GEMM that reads it; the forward kernel writes that bf16 copy itself
     (``y._gd_bf16``, read by wgrad.TokenLinear) for one extra 2-byte store
     per element instead of a cast kernel per consumer."""
-    return (TWIN and x.is_cuda and torch.is_autocast_enabled("cuda")
+    return (wanted and TWIN and x.is_cuda and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16)
 
 
@@ -57,14 +57,14 @@ def _workspace(c, device):
 
 class AddLayerNormFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps):
+    def forward(ctx, x, r, weight, bias, eps, twin=True):
         c = x.shape[-1]
         rows = x.numel() // c
         y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         mean = torch.empty(rows, dtype=torch.float32, device=x.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
         rd = x if r is None else r  # r None: LayerNorm(x) alone (NULL residual)
-        y16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if _bf16_twin_wanted(x) else None
+        y16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if _bf16_twin_wanted(x, twin) else None
         _lib.call("gd_add_layernorm_forward2", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(rd), _lib.ptr(r),
                   weight.data_ptr(), bias.data_ptr(), rows, c, float(eps), y.data_ptr(), _lib.ptr(y16),
                   mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(x),
@@ -94,22 +94,25 @@ class AddLayerNormFunction(torch.autograd.Function):
                   nbytes=rows * (c * (2 * x.element_size() + (0 if r is None else r.element_size()) + 4
                                       + (r.element_size() if dr is not None else 0)) + 8))
         return (dx if ctx.needs_input_grad[0] else None, dr, dw if ctx.needs_input_grad[2] else None,
-                db if ctx.needs_input_grad[3] else None, None)
+                db if ctx.needs_input_grad[3] else None, None, None)
 
 
-def layer_norm(norm: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+def layer_norm(norm: nn.LayerNorm, x: torch.Tensor, bf16_twin: bool = True) -> torch.Tensor:
     """norm(x) with no residual (Swin's pre-norms and patch-merging norm,
     swin_transformer.py:245, 296, 357): the same kernels with a NULL residual,
-    fp32 output as autocast's LayerNorm; elsewhere nn.LayerNorm."""
+    fp32 output as autocast's LayerNorm; elsewhere nn.LayerNorm.
+    ``bf16_twin``: the output feeds a GEMM (TokenLinear reads the twin);
+    False where it does not (a permute / copy), to skip the extra store."""
     if supported(norm, x, None):
-        return AddLayerNormFunction.apply(x.contiguous(), None, norm.weight, norm.bias, norm.eps)
+        return AddLayerNormFunction.apply(x.contiguous(), None, norm.weight, norm.bias, norm.eps, bool(bf16_twin))
     return norm(x)
 
 
-def add_norm(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
-    """norm(x + r)"""
+def add_norm(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, bf16_twin: bool = True) -> torch.Tensor:
+    """norm(x + r); ``bf16_twin`` as in layer_norm"""
     if supported(norm, x, r):
         # (the decoder's MSDA output arrives transposed: one copy, which the
         # unfused add would pay as well)
-        return AddLayerNormFunction.apply(x.contiguous(), r.contiguous(), norm.weight, norm.bias, norm.eps)
+        return AddLayerNormFunction.apply(x.contiguous(), r.contiguous(), norm.weight, norm.bias, norm.eps,
+                                          bool(bf16_twin))
     return norm(x + r)

@@ -187,7 +187,11 @@ class _AddScaled(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, branch, s):
-        ctx.save_for_backward(branch, s)
+        # the branch is only needed for d s (a layer-scale gamma); a drop-path
+        # mask needs no gradient, and keeping the branch alive until backward
+        # would hold one activation per residual for nothing
+        ctx.save_for_backward(branch if ctx.needs_input_grad[2] else None, s)
+        ctx.branch_meta = (branch.shape, branch.dtype)
         with torch.autocast(device_type=x.device.type, enabled=False):
             return torch.addcmul(x, branch, s)
 
@@ -196,7 +200,8 @@ class _AddScaled(torch.autograd.Function):
         branch, s = ctx.saved_tensors
         gb = gs = None
         if ctx.needs_input_grad[1]:
-            gb = torch.empty(branch.shape, dtype=branch.dtype, device=branch.device)
+            shape, dtype = ctx.branch_meta
+            gb = torch.empty(shape, dtype=dtype, device=g.device)
             torch.mul(g, s, out=gb)
         if ctx.needs_input_grad[2]:
             c = g.shape[-1]

@@ -1,0 +1,154 @@
+"""The whole Grounding DINO train step as ONE HIP graph.
+
+Round 3 captured forward_core and its backward (gdino_amd.graphs) and ran the
+criterion and the optimizer eagerly between the replays.  The criterion's
+Hungarian matching needed the host (one device->host copy, a host wait for
+the forward, scipy, then the post-matching loss launches), so every step
+serialised there, and the eager launches between the replays left the
+device idle about 13 ms per step.  With the matching on the device
+(gdino_amd.lsap, scipy's algorithm) nothing in the step needs the host, so
+the step is captured whole and replayed with one launch:
+
+    forward_core -> SetCriterion.loss_prepared (cost matrices, device LSA,
+    token focal / L1 / GIoU) -> weighted sum -> backward (+ the bucketed
+    RCCL gradient all-reduce overlapped with it, train.BucketedGradSync, for
+    N > 1) -> clip_grad_norm_ -> fused AdamW (capturable, lr as a device
+    tensor so the LR scheduler still acts on replays).
+
+The host side per step is the text tokenisation and the target packing
+(SetCriterion.prepare_targets: positive maps, padded targets), both copied
+asynchronously into the graph's static input buffers.  A graph is captured
+per batch signature (image size, text length, padded target count); the
+target count is padded to a multiple of ``kmax_multiple`` so batches with
+different numbers of boxes share a graph (the padded pair slots are masked
+exactly in loss_prepared).
+
+Reference: the step engine_multi.py:499-564 / main.py:254-292 run eagerly.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import castcache
+from .train import BucketedGradSync, weighted_loss
+
+
+def _static_like(t: torch.Tensor) -> torch.Tensor:
+    return torch.empty_like(t, memory_format=torch.contiguous_format)
+
+
+class _Captured:
+    def __init__(self):
+        self.graph = torch.cuda.CUDAGraph()
+        self.inputs = {}
+        self.loss = None
+        self.loss_dict = None
+
+    def load(self, inputs):
+        for k, v in inputs.items():
+            self.inputs[k].copy_(v, non_blocking=True)
+
+
+class TrainStepGraph:
+    """Callable like train.train_step(samples, targets, captions, cat_lists)
+    -> loss tensor, replaying a captured whole-step graph.
+
+    ``warmup`` eager iterations (full optimizer steps, on a side stream)
+    precede each capture: they initialise the library handles, the weight
+    shadows / cast caches, the criterion's index caches and, for N > 1, the
+    gradient buckets."""
+
+    def __init__(self, model, criterion, optimizer, clip_max_norm: float = 0.1, amp_dtype=torch.bfloat16,
+                 grad_sync: BucketedGradSync | None = None, warmup: int = 2, kmax_multiple: int = 8):
+        self.model, self.criterion, self.optimizer = model, criterion, optimizer
+        self.clip_max_norm, self.amp_dtype = clip_max_norm, amp_dtype
+        self.grad_sync, self.warmup, self.kmax_multiple = grad_sync, warmup, kmax_multiple
+        self.graphs = {}
+        self.captures = 0
+        device = next(model.parameters()).device
+        for g in optimizer.param_groups:  # capturable fused AdamW; lr a device tensor the scheduler fills
+            g["capturable"] = True
+            if not torch.is_tensor(g["lr"]):
+                g["lr"] = torch.tensor(float(g["lr"]), dtype=torch.float32, device=device)
+
+    # ------------------------------------------------------------ inputs
+    def _prepare(self, samples, targets, captions, cat_lists):
+        model = self.model
+        device = samples.tensors.device
+        text, token = model.prepare_text(captions, device)
+        k = max(max((len(t["labels"]) for t in targets), default=0), 1)
+        k = -(-k // self.kmax_multiple) * self.kmax_multiple
+        prep = self.criterion.prepare_targets(targets, cat_lists, captions, token, device, kmax=k)
+        inputs = {"images": samples.tensors, "mask": samples.mask}
+        for n in ("input_ids", "token_type_ids", "text_token_mask", "self_masks", "position_ids"):
+            inputs[n] = text[n]
+        for n in ("tgt_boxes", "maps", "valid", "sizes", "num_boxes"):
+            inputs[n] = prep[n]
+        return inputs
+
+    @staticmethod
+    def _signature(inputs):
+        return tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(inputs.items()))
+
+    # -------------------------------------------------------------- step
+    def _body(self, inp):
+        """forward + loss + backward + all-reduce + clip + optimizer step;
+        only device work, no host synchronisation."""
+        model, crit = self.model, self.criterion
+        dev_type = inp["images"].device.type
+        with torch.autocast(device_type=dev_type, dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
+            core = model.forward_core(inp["images"], inp["mask"], inp["input_ids"], inp["token_type_ids"],
+                                      inp["text_token_mask"], inp["self_masks"], inp["position_ids"])
+            outputs = model.assemble_outputs(core)
+            prep = {n: inp[n] for n in ("tgt_boxes", "maps", "valid", "sizes", "num_boxes")}
+            loss_dict, _ = crit.loss_prepared(outputs, prep)
+            loss = weighted_loss(loss_dict, crit.weight_dict)
+        if self.grad_sync is not None:
+            self.grad_sync.zero_grad()
+        loss.backward()
+        if self.grad_sync is not None:
+            self.grad_sync.after_backward()
+        if self.clip_max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), self.clip_max_norm, foreach=True)
+        self.optimizer.step()
+        return loss.detach(), {k: v.detach() for k, v in loss_dict.items()}
+
+    def _capture(self, key, inputs):
+        c = _Captured()
+        for k, v in inputs.items():
+            c.inputs[k] = _static_like(v)
+        c.load(inputs)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                if self.grad_sync is None:
+                    self.optimizer.zero_grad(set_to_none=True)
+                self._body(c.inputs)
+        torch.cuda.current_stream().wait_stream(side)
+        if self.grad_sync is None:
+            # the captured backward allocates the gradients from the graph's
+            # pool; every replay rewrites them in place
+            self.optimizer.zero_grad(set_to_none=True)
+        # (a private memory pool per graph: a shared one would let a later
+        # capture reuse memory an earlier graph's replays still write)
+        with torch.cuda.graph(c.graph):
+            c.loss, c.loss_dict = self._body(c.inputs)
+        self.graphs[key] = c
+        self.captures += 1
+        return c
+
+    def __call__(self, samples, targets, captions, cat_lists):
+        inputs = self._prepare(samples, targets, captions, cat_lists)
+        key = self._signature(inputs)
+        c = self.graphs.get(key)
+        if c is None:
+            c = self._capture(key, inputs)
+        else:
+            c.load(inputs)
+        c.graph.replay()
+        castcache._on_optimizer_step()  # the replay stepped the optimizer: cast copies are stale
+        return c.loss
+
+    def release(self):
+        self.graphs.clear()

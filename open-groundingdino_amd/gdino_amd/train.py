@@ -195,19 +195,154 @@ class GradAllReduce:
             bucket, size = ([g], g.numel() * g.element_size()) if g is not None else ([], 0)
 
 
+class BucketedGradSync:
+    """Data-parallel gradient averaging overlapped with the backward pass --
+    DDP's reducer (reference main.py:258-261) restated so that it also runs
+    INSIDE a captured HIP graph (gdino_amd.stepgraph), where DDP's own
+    bookkeeping cannot follow replays.
+
+    * Buckets follow the order in which the backward finishes gradients
+      (recorded in the first backward, as DDP rebuilds its buckets after the
+      first iteration); a bucket holds up to ``bucket_mb`` of gradients, the
+      first one ``first_bucket_mb`` so the first collective starts early.
+    * Each trainable parameter's ``.grad`` is a view into its bucket's flat
+      buffer (DDP's gradient_as_bucket_view): the backward accumulates
+      straight into the buffer, and there is no flatten / unflatten copy.
+    * A post-accumulate-grad hook counts a bucket's ready gradients; the last
+      one divides the bucket by the world size and issues its RCCL
+      all-reduce (async, on the process group's communication stream) while
+      the backward goes on producing the next buckets.  A callback at the end
+      of the backward waits for every bucket (the current stream waits on the
+      communication stream: no host block on the GPU).
+    * ``zero_grad()`` replaces optimizer.zero_grad(set_to_none=True), which
+      would drop the views.
+    Same averaged gradients as DDP (tests/test_ddp_gloo.py).  Parameters that
+    receive no gradient in the recording backward keep ``.grad = None``."""
+
+    def __init__(self, params, bucket_mb: float = 25, first_bucket_mb: float = 1, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.params = [p for p in params if p.requires_grad]
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.first_bytes = int(first_bucket_mb * (1 << 20))
+        self.order = []          # grad-ready order seen by the recording backward
+        self.buckets = None      # [{"flat", "params", "pending", "work"}]
+        self.bucket_of = {}
+        self._queued = False
+        self._handles = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
+
+    # ---------------------------------------------------------------- hooks
+    def _ready(self, p):
+        if self.buckets is None:
+            self.order.append(p)
+            return
+        if not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        b = self.bucket_of.get(id(p))
+        if b is None:
+            return
+        b["pending"] -= 1
+        if b["pending"] == 0:
+            self._launch(b)
+
+    def _launch(self, b):
+        b["flat"].div_(self.world)
+        b["work"] = self.dist.all_reduce(b["flat"], group=self.group, async_op=True)
+
+    def _finalize(self):
+        for b in self.buckets:
+            if b["work"] is None:  # a parameter without gradient this pass
+                self._launch(b)
+        for b in self.buckets:
+            b["work"].wait()
+            b["work"] = None
+            b["pending"] = len(b["params"])
+        self._queued = False
+
+    # ------------------------------------------------------------ lifecycle
+    def _build(self):
+        """Buckets over the recorded order; grads move into the flat buffers."""
+        seen, order = set(), []
+        for p in self.order:
+            if id(p) not in seen and p.grad is not None:
+                seen.add(id(p))
+                order.append(p)
+        self.buckets, cur, size = [], [], 0
+        for p in order:
+            nbytes = p.numel() * 4
+            cap = self.first_bytes if not self.buckets else self.bucket_bytes
+            if cur and (size + nbytes > cap or p.dtype != cur[0].dtype):
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += nbytes
+        if cur:
+            self.buckets.append(cur)
+        built = []
+        for ps in self.buckets:
+            flat = torch.zeros(sum(p.numel() for p in ps), dtype=ps[0].dtype, device=ps[0].device)
+            off = 0
+            for p in ps:
+                view = flat[off:off + p.numel()].view_as(p)
+                view.copy_(p.grad)
+                p.grad = view
+                off += p.numel()
+            b = {"flat": flat, "params": ps, "pending": len(ps), "work": None}
+            built.append(b)
+            for p in ps:
+                self.bucket_of[id(p)] = b
+        self.buckets = built
+
+    def after_backward(self):
+        """Call after every backward (train_step does): the recording pass
+        all-reduces its gradients in one go and builds the buckets; later
+        passes were already reduced by the hooks."""
+        if self.buckets is not None:
+            return
+        self._build()
+        for b in self.buckets:
+            self._launch(b)
+        for b in self.buckets:
+            b["work"].wait()
+            b["work"] = None
+
+    def zero_grad(self):
+        if self.buckets is None:
+            for p in self.params:
+                p.grad = None
+        else:
+            for b in self.buckets:
+                b["flat"].zero_()
+
+    def bucket_sizes_mb(self):
+        return [b["flat"].numel() * b["flat"].element_size() / 2 ** 20 for b in (self.buckets or [])]
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+
+
 def train_step(model, criterion, optimizer, samples, targets, captions, cat_lists, clip_max_norm=0.1,
                amp_dtype=torch.bfloat16, grad_sync=None):
     """One optimisation step; returns the weighted loss tensor (not synced).
-    ``grad_sync``: called between backward and clipping (GradAllReduce in
-    the multi-GPU HIP-graph step)."""
+    ``grad_sync``: a BucketedGradSync (all-reduce overlapped with the
+    backward; its after_backward() is called) or a plain callable run
+    between backward and clipping (GradAllReduce)."""
     dev_type = samples.tensors.device.type
     with torch.autocast(device_type=dev_type, dtype=amp_dtype, enabled=amp_dtype is not None):
         outputs = model(samples, captions=captions)
         loss_dict = criterion(outputs, targets, cat_lists, captions)
         loss = weighted_loss(loss_dict, criterion.weight_dict)
-    optimizer.zero_grad(set_to_none=True)
+    if isinstance(grad_sync, BucketedGradSync):
+        grad_sync.zero_grad()
+    else:
+        optimizer.zero_grad(set_to_none=True)
     loss.backward()
-    if grad_sync is not None:
+    if isinstance(grad_sync, BucketedGradSync):
+        grad_sync.after_backward()
+    elif grad_sync is not None:
         grad_sync()
     if clip_max_norm > 0:
         torch.nn.utils.clip_grad_norm_(model.parameters(), clip_max_norm, foreach=True)

@@ -344,7 +344,7 @@ class SwinTransformer(nn.Module):
         for i, layer in enumerate(self.layers):
             x_out, h, w, x, wh, ww = layer(x, wh, ww)
             if i in self.out_indices:
-                y = layer_norm(getattr(self, f"norm{i}"), x_out)
+                y = layer_norm(getattr(self, f"norm{i}"), x_out, bf16_twin=False)  # feeds a permute, not a GEMM
                 outs.append(y.view(-1, h, w, self.num_features[i]).permute(0, 3, 1, 2).contiguous())
         return outs
 

@@ -68,6 +68,17 @@ def prepare_text_host(tokenizer, special_tokens, max_text_len, captions):
     return text, tokenized
 
 
+def to_device_async(t: torch.Tensor, device) -> torch.Tensor:
+    """Host tensor -> device without a stream synchronisation: a pageable
+    source copied with non_blocking=False makes torch wait for the whole
+    stream (the queued forward included) before the copy; staging it through
+    pinned memory (torch's caching host allocator) keeps the copy async."""
+    device = torch.device(device)
+    if device.type != "cuda" or t.device.type != "cpu":
+        return t.to(device)
+    return (t if t.is_pinned() else t.pin_memory()).to(device, non_blocking=True)
+
+
 class GroundingDINO(nn.Module):
     def __init__(self, backbone, transformer, num_queries, aux_loss=False, iter_update=False, query_dim=2,
                  num_feature_levels=1, nheads=8, two_stage_type="no", dec_pred_bbox_embed_share=True,
@@ -169,7 +180,7 @@ class GroundingDINO(nn.Module):
         -> (dict of device tensors, tokenizer output for the loss)."""
         text, tokenized = prepared if prepared is not None else prepare_text_host(
             self.tokenizer, self.specical_tokens, self.max_text_len, captions)
-        return {k: v.to(device, non_blocking=v.is_pinned()) for k, v in text.items()}, tokenized
+        return {k: to_device_async(v, device) for k, v in text.items()}, tokenized
 
     def encode_text(self, input_ids, token_type_ids, text_token_mask, self_masks, position_ids):
         """BERT + feat_map -> text_dict (groundingdino.py:259-287)."""
@@ -235,9 +246,14 @@ class GroundingDINO(nn.Module):
         device = samples.tensors.device
         text, one_hot_token = self.prepare_text(captions, device, kw.get("prepared_text"))
         core = self._graphed_core if getattr(self, "_graphed_core", None) is not None else self.forward_core
+        outs = core(samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
+                    text["text_token_mask"], text["self_masks"], text["position_ids"])
+        return self.assemble_outputs(outs, one_hot_token)
+
+    def assemble_outputs(self, core_outputs, one_hot_token=None):
+        """forward_core's tuple -> the reference output dict (:343-392)."""
         (outputs_class, outputs_coord, text_mask, interm_class, interm_coord,
-         init_box_proposal) = core(samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
-                                   text["text_token_mask"], text["self_masks"], text["position_ids"])
+         init_box_proposal) = core_outputs
         out = {"pred_logits": outputs_class[-1], "pred_boxes": outputs_coord[-1], "text_mask": text_mask}
         if self.aux_loss:
             out["aux_outputs"] = self._set_aux_loss(outputs_class, outputs_coord)
@@ -329,20 +345,33 @@ class SetCriterion(nn.Module):
                 oh[i, src.to(device)] = label_maps[i].to(device)[lab].long()
         return oh
 
+    @staticmethod
+    def _heads(outputs):
+        heads = [("", outputs)]
+        for i, aux in enumerate(outputs.get("aux_outputs", [])):
+            heads.append((f"_{i}", aux))
+        if "interm_outputs" in outputs:
+            heads.append(("_interm", outputs["interm_outputs"]))
+        return heads
+
     def forward(self, outputs, targets, cat_list, caption, return_indices=False):
         device = outputs["pred_logits"].device
+        heads = self._heads(outputs)
+        if self._device_matching_ok(heads, targets):
+            # matching on the device (gdino_amd.lsap): no device->host copy,
+            # no host wait anywhere in the loss
+            prep = self.prepare_targets(targets, cat_list, caption, outputs["token"], device)
+            losses, pairs = self.loss_prepared(outputs, prep)
+            if return_indices:
+                indices_list = self._pairs_to_indices(pairs, prep["sizes"], len(heads))
+                return losses, indices_list[1:] + indices_list[:1]
+            return losses
         token = outputs["token"]
         bs = len(cat_list)
         label_maps = []
         for j in range(bs):
             label_maps.append(create_positive_map(token[j], range(len(cat_list[j])), cat_list[j], caption[j])
                               .to(device))
-
-        heads = [("", outputs)]
-        for i, aux in enumerate(outputs.get("aux_outputs", [])):
-            heads.append((f"_{i}", aux))
-        if "interm_outputs" in outputs:
-            heads.append(("_interm", outputs["interm_outputs"]))
 
         num_boxes = torch.as_tensor([float(sum(len(t["labels"]) for t in targets))], device=device)
         if is_dist_avail_and_initialized():
@@ -356,6 +385,157 @@ class SetCriterion(nn.Module):
         if return_indices:
             return losses, indices_list[1:] + indices_list[:1]
         return losses
+
+    # ---------------------------------------------------- device matching
+    # DEVICE_MATCHING = False: the host scipy path (_forward_batched) for A/B
+    DEVICE_MATCHING = True
+
+    def _device_matching_ok(self, heads, targets):
+        from gdino_amd import _lib, lsap
+        logits = heads[0][1]["pred_logits"]
+        kmax = max((len(t["labels"]) for t in targets), default=0)
+        return (self.DEVICE_MATCHING and self._can_batch(heads, targets) and _lib.on_device(logits)
+                and _lib.enabled("lsap") and getattr(self.matcher, "device_matching", False)
+                and lsap.supported(logits.shape[1], kmax))
+
+    def prepare_targets(self, targets, cat_list, caption, token, device, kmax=None):
+        """The host side of the loss (reference :553-574 before the matcher):
+        positive maps of every caption's categories, each target's token map,
+        targets padded to ``kmax`` (default: the batch maximum) -- all moved
+        with async copies, no stream synchronisation.  -> dict:
+          tgt_boxes [B, K, 4] f32, maps [B, K, 256] f32 (positive map of each
+          target's label), valid [B, K] bool, sizes [B] int32 (device),
+          num_boxes [1] f32 (device, this rank's target count), "sizes" is
+          also kept as a host list under "sizes_host"."""
+        bs = len(targets)
+        sizes = [len(t["labels"]) for t in targets]
+        k = max(max(sizes, default=0), 1) if kmax is None else int(kmax)
+        if max(sizes, default=0) > k:
+            raise ValueError(f"prepare_targets: {max(sizes)} targets > kmax {k}")
+        label_maps = [create_positive_map(token[j], range(len(cat_list[j])), cat_list[j], caption[j])
+                      for j in range(bs)]
+        cmax = max(max(m.shape[0] for m in label_maps), 1)
+        lm = torch.zeros(bs, cmax, label_maps[0].shape[1], dtype=torch.float32)
+        for j, m in enumerate(label_maps):
+            lm[j, :m.shape[0]] = m
+        valid = torch.as_tensor(np.arange(k)[None, :] < np.asarray(sizes)[:, None])
+        host = {"label_maps": lm, "valid": valid, "sizes": torch.as_tensor(sizes, dtype=torch.int32),
+                "num_boxes": torch.as_tensor([float(sum(sizes))], dtype=torch.float32)}
+        dev = {n: to_device_async(v, device) for n, v in host.items()}
+        tgt_boxes = torch.zeros(bs, k, 4, dtype=torch.float32, device=device)
+        labels = torch.zeros(bs, k, dtype=torch.int64, device=device)
+        for j, t in enumerate(targets):
+            n = sizes[j]
+            if n:
+                tgt_boxes[j, :n] = to_device_async(t["boxes"], device).float()
+                labels[j, :n] = to_device_async(t["labels"], device)
+        bidx = torch.arange(bs, device=device)[:, None].expand(bs, k)
+        dev["maps"] = dev.pop("label_maps")[bidx, labels]  # [B, K, 256]
+        dev["tgt_boxes"] = tgt_boxes
+        dev["sizes_host"] = sizes
+        return dev
+
+    def loss_prepared(self, outputs, prep):
+        """All heads' losses from prepare_targets' tensors, entirely on the
+        device and free of host synchronisation (static shapes: capturable
+        into the train-step HIP graph).  Same losses as _forward_batched
+        (reference :553-636): one cost pass for all H x B problems, the
+        Hungarian assignment of each on the device (gdino_amd.lsap, scipy's
+        algorithm and tie-breaking), token focal / L1 / GIoU on the matched
+        pairs.  Padded pair slots (images with fewer targets than K) are
+        masked out exactly.  -> (losses, (rows, cols) [H*B, K])."""
+        from gdino_amd import lsap
+        heads = self._heads(outputs)
+        device = outputs["pred_logits"].device
+        H = len(heads)
+        logits = torch.stack([o["pred_logits"] for _, o in heads])          # [H, B, Q, 256]
+        boxes = torch.stack([o["pred_boxes"] for _, o in heads])            # [H, B, Q, 4]
+        _, B, Q, _ = logits.shape
+        tgt_boxes, maps, valid, sizes = prep["tgt_boxes"], prep["maps"], prep["valid"], prep["sizes"]
+        K = maps.shape[1]
+
+        num_boxes = prep["num_boxes"].clone()
+        if is_dist_avail_and_initialized():
+            torch.distributed.all_reduce(num_boxes)
+        num_boxes = torch.clamp(num_boxes / get_world_size(), min=1)[0]
+
+        cost = self.matcher.cost_batched(logits, boxes, tgt_boxes, maps, valid)   # [H, B, Q, K]
+        rows, cols = lsap.linear_sum_assignment_batched(cost.reshape(H * B, Q, K), sizes.repeat(H))
+        w = (rows >= 0).view(-1)                                            # [H*B*K] real pairs
+        hi, bi = self._pair_heads(H, B, K, device)
+        qi = rows.clamp(min=0).view(-1)
+        ki = cols.clamp(min=0).view(-1)
+        npos = torch.clamp(torch.minimum(sizes, torch.full_like(sizes, Q)).sum().float(), min=1.0)
+
+        # token-level sigmoid focal loss (token_sigmoid_binary_focal_loss, :462-496); padded
+        # slots write their (zero) rows into a spare query row Q that is sliced off
+        t = torch.zeros((H, B, Q + 1, logits.shape[-1]), dtype=torch.float32, device=device)
+        t[hi, bi, torch.where(w, qi, torch.full_like(qi, Q))] = maps[bi, ki].float()
+        t = t[:, :, :Q]
+        keep = outputs["text_mask"][None, :, None, :]
+        x = torch.where(keep, logits.float(), torch.zeros((), device=device))
+        p = torch.sigmoid(x)
+        ce = F.binary_cross_entropy_with_logits(x, t, reduction="none")
+        p_t = p * t + (1 - p) * (1 - t)
+        fl = ce * ((1 - p_t) ** self.focal_gamma)
+        if self.focal_alpha >= 0:
+            fl = (self.focal_alpha * t + (1 - self.focal_alpha) * (1 - t)) * fl
+        loss_ce = torch.where(keep, fl, torch.zeros((), device=device)).sum((1, 2, 3)) / npos
+
+        # L1 + GIoU on the matched pairs (loss_boxes, :436-459); a padded slot
+        # compares against a unit dummy box (finite GIoU) and is zeroed by where
+        src = boxes[hi, bi, qi].float()
+        wc = w[:, None]
+        tgt = torch.where(wc, tgt_boxes[bi, ki].float(), torch.full((), 0.5, device=device))
+        l1 = torch.where(wc, (src - tgt).abs(), torch.zeros((), device=device))
+        giou = box_ops.paired_generalized_box_iou(box_ops.box_cxcywh_to_xyxy(src), box_ops.box_cxcywh_to_xyxy(tgt))
+        one_m = torch.where(w, 1 - giou, torch.zeros((), device=device))
+        zeros = torch.zeros(H, dtype=torch.float32, device=device)
+        loss_bbox = zeros.index_add(0, hi, l1.sum(-1)) / num_boxes
+        loss_giou = zeros.index_add(0, hi, one_m) / num_boxes
+        with torch.no_grad():
+            l1d = l1.detach()
+            loss_xy = zeros.index_add(0, hi, l1d[:, :2].sum(-1)) / num_boxes
+            loss_hw = zeros.index_add(0, hi, l1d[:, 2:].sum(-1)) / num_boxes
+
+        per = {"loss_ce": loss_ce.unbind(0), "loss_bbox": loss_bbox.unbind(0), "loss_giou": loss_giou.unbind(0),
+               "loss_xy": loss_xy.unbind(0), "loss_hw": loss_hw.unbind(0)}
+        order = (["loss_ce"] if "labels" in self.losses else []) + \
+                (["loss_bbox", "loss_giou", "loss_xy", "loss_hw"] if "boxes" in self.losses else [])
+        losses = {}
+        for h, (suffix, o) in enumerate(heads):
+            for k in order:
+                losses[k + suffix] = per[k][h]
+            if suffix:
+                o["text_mask"] = outputs["text_mask"]
+        return losses, (rows, cols)
+
+    _PAIR_IDX: dict = {}
+
+    @classmethod
+    def _pair_heads(cls, H, B, K, device):
+        """head / image index of every pair slot ([H*B*K] each, cached)"""
+        key = (H, B, K, str(device))
+        v = cls._PAIR_IDX.get(key)
+        if v is None:
+            hb = torch.arange(H * B * K) // K
+            v = cls._PAIR_IDX[key] = (to_device_async(hb // B, device), to_device_async(hb % B, device))
+        return v
+
+    @staticmethod
+    def _pairs_to_indices(pairs, sizes, H):
+        """device (rows, cols) -> the reference's [[(src, tgt)] * B] * H host lists"""
+        rows, cols = (x.cpu() for x in pairs)
+        B = len(sizes)
+        out = []
+        for h in range(H):
+            per = []
+            for b in range(B):
+                r, c = rows[h * B + b], cols[h * B + b]
+                m = r >= 0
+                per.append((r[m].clone(), c[m].clone()))
+            out.append(per)
+        return out
 
     def _forward_per_head(self, heads, outputs, targets, label_maps, num_boxes, device):
         """The reference's loop (groundingdino.py:553-636): per head, match,
@@ -382,7 +562,7 @@ class SetCriterion(nn.Module):
 
     def _can_batch(self, heads, targets):
         shp_l, shp_b = heads[0][1]["pred_logits"].shape, heads[0][1]["pred_boxes"].shape
-        return (set(self.losses) <= {"labels", "boxes"} and hasattr(self.matcher, "match_batched")
+        return (set(self.losses) <= {"labels", "boxes"} and getattr(self.matcher, "batched", False)
                 and all(o["pred_logits"].shape == shp_l and o["pred_boxes"].shape == shp_b for _, o in heads)
                 and max((len(t["labels"]) for t in targets), default=0) > 0)
 

@@ -34,6 +34,11 @@ def _focal_token_cost(logits, label_map, alpha, gamma):
 
 
 class HungarianMatcher(nn.Module):
+    # SetCriterion may batch all heads' problems (match_batched) and match on
+    # the device (gdino_amd.lsap: scipy's algorithm)
+    batched = True
+    device_matching = True
+
     def __init__(self, cost_class: float = 1, cost_bbox: float = 1, cost_giou: float = 1, focal_alpha=0.25):
         super().__init__()
         self.cost_class = cost_class
@@ -134,6 +139,8 @@ class HungarianMatcher(nn.Module):
 
 class SimpleMinsumMatcher(HungarianMatcher):
     """Per-target argmin over queries (reference matcher.py:123-201)."""
+    batched = False  # match_batched / the device solver are Hungarian
+    device_matching = False
 
     @torch.no_grad()
     def forward(self, outputs, targets, label_map=None):

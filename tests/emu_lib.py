@@ -56,6 +56,7 @@ def lib():
         _LIB.gd_wgrad_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_add_layernorm_forward.argtypes = [_i, _p, _i, _p, _p, _p, _i64, _i, ctypes.c_float, _p, _p, _p, _p]
         _LIB.gd_add_layernorm_backward.argtypes = [_i, _p, _i, _p, _p, _p, _p, _p, _i64, _i] + [_p] * 6
+        _LIB.gd_linear_sum_assignment.argtypes = [_p, _i, _i, _i, _i64, _p, _p, _p, _p, _p]
         _LIB.gd_add_layernorm_workspace_bytes.argtypes = [_i]
         _LIB.gd_add_layernorm_workspace_bytes.restype = ctypes.c_size_t
         _LIB.gd_last_error.restype = ctypes.c_char_p
@@ -380,3 +381,17 @@ def attn_dropout_keep(B, H, Lq, Lk, p, seed):
 def rel_err(a, b):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def linear_sum_assignment(cost, sizes):
+    """cost [P, Q, K] f32, sizes [P] int -> (rows, cols, status) as the device
+    gd_linear_sum_assignment writes them"""
+    cost = cost.float().contiguous()
+    P, Q, K = cost.shape
+    sizes = torch.as_tensor(sizes, dtype=torch.int32).contiguous()
+    rows = torch.full((P, K), 7777, dtype=torch.int64)
+    cols = torch.full((P, K), 7777, dtype=torch.int64)
+    status = torch.full((P,), 7, dtype=torch.int32)
+    _check(lib().gd_linear_sum_assignment(_ptr(cost), P, Q, K, Q * K, _ptr(sizes), _ptr(rows), _ptr(cols),
+                                          _ptr(status), None))
+    return rows, cols, status

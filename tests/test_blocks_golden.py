@@ -44,19 +44,33 @@ def test_fused_projections_match_reference_fp64(name, monkeypatch):
     assert errs
 
 
-@pytest.mark.parametrize("batched", [True, False])
-def test_criterion_matches_reference_fp32(batched, monkeypatch):
+@pytest.mark.parametrize("path", ["device", "batched", "per_head"])
+def test_criterion_matches_reference_fp32(path, monkeypatch):
     """SetCriterion + HungarianMatcher (groundingdino.py:405-639,
     matcher.py:47-120): every loss term of the final, aux and interm heads
-    and the gradients w.r.t. logits and boxes, fp32 as in training.  Both the
-    all-heads-batched path (default) and the reference-shaped per-head loop."""
+    and the gradients w.r.t. logits and boxes, fp32 as in training.  Three
+    paths: "device" -- the default on the GPU: matching by the device
+    Hungarian kernel (csrc/lsap.hip, here on the host-side emulator) and the
+    sync-free masked loss (loss_prepared); "batched" -- all heads' cost
+    matrices in one pass, scipy on the host; "per_head" -- the
+    reference-shaped loop."""
+    import contextlib
     from models.GroundingDINO.groundingdino import SetCriterion
     taken = []
-    orig = SetCriterion._can_batch
-    monkeypatch.setattr(SetCriterion, "_can_batch",
-                        lambda self, h, t: taken.append(batched and orig(self, h, t)) or taken[-1])
-    errs = compare("criterion", "cpu", torch.float32, tol=1e-5, grad_tol=1e-5)
-    assert taken == [batched]
+    for name in ("loss_prepared", "_forward_batched", "_forward_per_head"):
+        orig = getattr(SetCriterion, name)
+        monkeypatch.setattr(SetCriterion, name,
+                            (lambda o, n: lambda self, *a, **k: taken.append(n) or o(self, *a, **k))(orig, name))
+    if path == "per_head":
+        monkeypatch.setattr(SetCriterion, "_can_batch", lambda self, h, t: False)
+    ctx = contextlib.nullcontext()
+    if path == "device":
+        from emu_product import emulated_product
+        ctx = emulated_product()
+    with ctx:
+        errs = compare("criterion", "cpu", torch.float32, tol=1e-5, grad_tol=1e-5)
+    assert taken == [{"device": "loss_prepared", "batched": "_forward_batched",
+                      "per_head": "_forward_per_head"}[path]]
     assert errs["total"] < 1e-5
 
 

@@ -74,10 +74,13 @@ def test_ddp_two_ranks_gloo():
 
 
 def _worker_grad_allreduce(rank, world, port, q):
-    """GradAllReduce (the multi-GPU HIP-graph step's gradient averaging)
-    against DDP on the same model, batches and seeds: identical gradients
-    (DDP also averages over ranks) after one step, small buckets so the
-    bucket boundaries are exercised."""
+    """GradAllReduce (post-backward) and BucketedGradSync (overlapped with
+    the backward: per-bucket all-reduces issued from post-accumulate hooks,
+    gradients as views of the bucket buffers -- the multi-GPU HIP-graph
+    step's gradient averaging) against DDP on the same model, batches and
+    seeds: identical gradients (DDP also averages over ranks), small buckets
+    so the bucket boundaries are exercised.  Two steps each (lr 0): the
+    first backward records the bucket order, the second runs overlapped."""
     sys.path[:0] = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "open-groundingdino_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -85,12 +88,13 @@ def _worker_grad_allreduce(rank, world, port, q):
     try:
         from oracle_hooks import oracle_msda
         from gdino_amd.config import make_args
-        from gdino_amd.train import GradAllReduce, build_training, synthetic_batch, train_step
+        from gdino_amd.train import BucketedGradSync, GradAllReduce, build_training, synthetic_batch, train_step
         args = make_args(device="cpu", num_queries=50, enc_layers=2, dec_layers=2)
         samples, targets, caps, cats = synthetic_batch(1, 96, 128, n_boxes=2, n_tokens=20, seed=200 + rank,
                                                        device="cpu")
         grads = {}
-        for mode in ("ddp", "manual"):
+        nb = 0
+        for mode in ("ddp", "manual", "bucketed"):
             torch.manual_seed(0)
             model, criterion, _, opt = build_training(args, "cpu")
             for m in model.modules():  # the same function in both runs
@@ -101,13 +105,23 @@ def _worker_grad_allreduce(rank, world, port, q):
             opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=0.0)
             if mode == "ddp":
                 net, sync = torch.nn.parallel.DistributedDataParallel(model), None
-            else:
+            elif mode == "manual":
                 net, sync = model, GradAllReduce(model.parameters(), bucket_mb=1)
+            else:
+                net, sync = model, BucketedGradSync(model.parameters(), bucket_mb=1, first_bucket_mb=0.25)
             with oracle_msda():
-                train_step(net, criterion, opt, samples, targets, caps, cats, amp_dtype=None, clip_max_norm=0.0,
-                           grad_sync=sync)
+                for _ in range(2):
+                    train_step(net, criterion, opt, samples, targets, caps, cats, amp_dtype=None,
+                               clip_max_norm=0.0, grad_sync=sync)
             grads[mode] = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None])
-        q.put((rank, float((grads["ddp"] - grads["manual"]).abs().max()), float(grads["ddp"].abs().max())))
+            if mode == "bucketed":
+                nb = len(sync.buckets)
+                # every gradient lives in a bucket buffer (no flatten copies)
+                assert all(any(p.grad.data_ptr() >= b["flat"].data_ptr() and
+                               p.grad.data_ptr() < b["flat"].data_ptr() + b["flat"].numel() * 4
+                               for b in sync.buckets) for p in model.parameters() if p.grad is not None)
+        q.put((rank, max(float((grads["ddp"] - grads[m]).abs().max()) for m in ("manual", "bucketed")),
+               float(grads["ddp"].abs().max()), nb))
     finally:
         dist.destroy_process_group()
 
@@ -123,5 +137,6 @@ def test_grad_allreduce_matches_ddp_two_ranks_gloo():
         p.join(timeout=600)
     res = sorted(q.get(timeout=5) for _ in range(2))
     assert all(p.exitcode == 0 for p in procs)
-    for _, diff, scale in res:
+    for _, diff, scale, nb in res:
         assert diff <= 1e-6 * max(scale, 1.0), res
+        assert nb > 3, res  # several buckets: boundaries exercised

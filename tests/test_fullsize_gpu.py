@@ -24,6 +24,18 @@ rounding of loc * W - 0.5 (DESIGN.md section 3, "Validation without a GPU");
 the sampling_offsets weights are perturbed by N(0, 0.01^2) (~0.2 px) so the
 gradient comparison is taken at a generic point, the same in every run.
 
+Box heads.  The last layers of the bbox MLPs are zero at init
+(groundingdino.py:170-171; enc_out_bbox_embed copies them, :193-195), so
+at init every predicted box IS its reference / proposal box and a box
+comparison checks no refinement arithmetic.  Every all-zero bbox-head
+parameter is perturbed by a seeded N(0, 0.01^2) as well (the same in every
+run): the box rows then compare the refinement chain (MLP, inverse sigmoid,
+add, sigmoid, the iterative reference update) in bf16.
+
+Verdicts.  Every compared row is recorded with both rules: the north_star's
+flat 1e-2 ("flat_ok") and the relaxed "within 1.5 x the reference's own
+bf16 error" ("rule_ok", what the assertion uses).
+
 Criterion (north_star: 1e-2 bf16).  bf16 autocast itself moves the outputs
 by err(C, F) (a few 1e-2 after 6 fusion + 6 encoder + 6 decoder layers), so
 "P matches the reference within 1e-2 bf16" is tested as: P's error against
@@ -44,18 +56,19 @@ TOL = 1e-2
 BF16_RATIO = 1.5
 
 
-def _build(backbone="swin_T_224_1k", seed=0, perturb_offsets=False):
+def _build(backbone="swin_T_224_1k", seed=0, perturb_offsets=False, perturb_boxes=True):
     from gdino_amd.config import make_args
     from gdino_amd.train import build_training
     torch.manual_seed(seed)
     args = make_args(device=DEV, backbone=backbone)
     model, criterion, _, opt = build_training(args, torch.device(DEV))
-    if perturb_offsets:
-        g = torch.Generator(device=DEV).manual_seed(seed + 1)
-        with torch.no_grad():
-            for n, p in model.named_parameters():
-                if "sampling_offsets.weight" in n:
-                    p.add_(torch.randn(p.shape, generator=g, device=DEV) * 0.01)
+    g = torch.Generator(device=DEV).manual_seed(seed + 1)
+    with torch.no_grad():
+        for n, p in model.named_parameters():  # (shared parameters listed once)
+            if perturb_offsets and "sampling_offsets.weight" in n:
+                p.add_(torch.randn(p.shape, generator=g, device=DEV) * 0.01)
+            if perturb_boxes and "bbox_embed" in n and not p.any():
+                p.add_(torch.randn(p.shape, generator=g, device=DEV) * 0.01)
     return model, criterion, opt
 
 
@@ -75,7 +88,8 @@ def _record_margins(test, rows):
     os.makedirs(os.path.dirname(MARGINS), exist_ok=True)
     with open(MARGINS, "a") as f:
         f.write(json.dumps({"test": test, "tol": TOL, "bf16_ratio": BF16_RATIO,
-                            "rows": [{"name": n, "P": p, "C": c} for n, p, c in rows]}) + "\n")
+                            "rows": [{"name": n, "P": p, "C": c, "flat_ok": p <= TOL,
+                                      "rule_ok": p <= max(TOL, BF16_RATIO * c)} for n, p, c in rows]}) + "\n")
 
 
 class PinnedMatch:
@@ -101,13 +115,27 @@ class PinnedMatch:
 
     @contextlib.contextmanager
     def active(self, mode):
+        from gdino_amd import lsap
         self.mode, self.calls = mode, 0
         names = [n for n in ("match_batched", "match_many") if hasattr(type(self.m), n)]
         for n in names:
             setattr(self.m, n, self._wrap(n))
+        # the device matching (SetCriterion.loss_prepared -> gdino_amd.lsap)
+        orig_lsa = lsap.linear_sum_assignment_batched
+
+        def lsa(*a, **k):
+            if self.mode == "record":
+                r = orig_lsa(*a, **k)
+                self.rec.append(r)
+                return r
+            r = self.rec[self.calls]
+            self.calls += 1
+            return r
+        lsap.linear_sum_assignment_batched = lsa
         try:
             yield
         finally:
+            lsap.linear_sum_assignment_batched = orig_lsa
             for n in names:
                 delattr(self.m, n)
 
