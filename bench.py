@@ -9,8 +9,9 @@ A step is one full training iteration of BASELINE config 3 (the metric's
 with 256-token captions, forward (Swin-T, BERT-base, 6+6 layer deformable
 transformer with fusion, 900 queries) -> SetCriterion (Hungarian matching,
 token focal + L1 + GIoU on 7 heads) -> backward -> clip_grad_norm(0.1) ->
-AdamW, under bf16 autocast, activation checkpointing as cfg_odvg, random
-weights.  Multi-GPU: one process per GPU, DDP over RCCL (all-reduce bucketed
+AdamW, under bf16 autocast, random weights; activation checkpointing off by
+default (--checkpointing on: cfg_odvg's recompute of the Swin blocks, fusion
+and encoder layers; same losses and gradients, see --checkpointing).  Multi-GPU: one process per GPU, DDP over RCCL (all-reduce bucketed
 and overlapped with backward), per-GPU batch fixed -> weak scaling.
 
 Rank 0 prints ONE JSON line with the contract fields plus
@@ -60,6 +61,11 @@ def parse(argv=None):
                          "the overlapped gradient all-reduce, clip, AdamW) as ONE HIP graph (default for the train "
                          "step on the GPU; DESIGN.md section 7)")
     ap.add_argument("--no-graphs", dest="graphs", action="store_false", help="eager train step")
+    ap.add_argument("--checkpointing", choices=("on", "off"), default="off",
+                    help="the reference's activation checkpointing (cfg_odvg use_checkpoint / use_transformer_ckpt: "
+                         "Swin blocks, fusion and encoder layers recomputed in the backward). Default off: the "
+                         "bs=2 step's activations fit a 288 GB MI355X many times over, and the loss and gradients "
+                         "are the same either way (train.set_activation_checkpointing)")
     ap.add_argument("--tunableop", default=None, metavar="CSV",
                     help="use pre-tuned hipBLASLt GEMM solutions from CSV (tools/tune_gemms.py); no tuning at run time")
     ap.add_argument("--output-dir", default=None,
@@ -128,7 +134,7 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(bs):
+def cpu_baseline(bs, recompute=False):
     """The reference's pure-PyTorch MSDA CPU fallback (oracle restatement of
     ms_deform_attn_core_pytorch, oracle/msda_torch.py) timed on this host by
     BASELINE.md section 3's protocol: cfg1 (N=1, 512x512 levels, Lq=100) fwd
@@ -137,8 +143,11 @@ def cpu_baseline(bs):
     with fewer reps (the encoder case is 0.4-2.5 s per call: 2 warmups + 5
     reps); median and p90 of each, at 1 thread and at the process's thread
     count.  `value` converts the all-thread medians to images/s of the train
-    step's MSDA share (6 encoder fwd recomputed under activation
-    checkpointing + 6 encoder fwd+bwd + 6 decoder fwd+bwd per step)."""
+    step's MSDA share (6 encoder fwd+bwd + 6 decoder fwd+bwd per step, plus
+    6 encoder fwd recomputed when the step runs with activation
+    checkpointing).  Thread counts: 1, the process's torch threads and the
+    affinity's full core count (all host cores); ``value`` is
+    the best of them, ``cores`` its thread count."""
     import statistics
 
     from oracle.msda_torch import msda_grid_sample
@@ -177,8 +186,12 @@ def cpu_baseline(bs):
     cases = [("cfg1_fwd", cfg1, False, 5, 20), ("cfg1_fwd_bwd", cfg1, True, 5, 20),
              ("enc_fwd", enc, False, 2, 5), ("enc_fwd_bwd", enc, True, 2, 5), ("dec_fwd_bwd", dec, True, 3, 10)]
     threads = torch.get_num_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
     res = {}
-    for nt in (threads, 1):
+    for nt in sorted({threads, 1, affinity}, reverse=True):
         torch.set_num_threads(nt)
         try:
             res[nt] = {name: timed(inp, bwd, w, r) for name, inp, bwd, w, r in cases}
@@ -186,25 +199,25 @@ def cpu_baseline(bs):
             torch.set_num_threads(threads)
 
     def per_step(r):
-        return 6 * (r["enc_fwd"]["median_s"] + r["enc_fwd_bwd"]["median_s"] + r["dec_fwd_bwd"]["median_s"])
+        return 6 * ((r["enc_fwd"]["median_s"] if recompute else 0.0) + r["enc_fwd_bwd"]["median_s"]
+                    + r["dec_fwd_bwd"]["median_s"])
 
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except AttributeError:
-        affinity = os.cpu_count()
+    best = min(res, key=lambda nt: per_step(res[nt]))
     return {
-        "value": bs / per_step(res[threads]),
+        "value": bs / per_step(res[best]),
         "unit": "images/s (MSDA fwd+bwd share of the train step only)",
-        "cores": threads,
+        "cores": best,
         "kind": "port",
+        "by_threads": {f"{nt}": round(bs / per_step(r), 4) for nt, r in res.items()},
         "single_thread": {"value": bs / per_step(res[1]), "cores": 1},
         "cases": {f"{nt}thr": {k: {kk: round(vv, 6) if isinstance(vv, float) else vv for kk, vv in d.items()}
                                for k, d in r.items()} for nt, r in res.items()},
         "sample": (f"reference pure-PyTorch MSDA fallback (grid_sample restatement, oracle/msda_torch.py) on "
                    f"{_cpu_model()}, torch threads={threads}, affinity cpus={affinity}, "
                    f"os.cpu_count()={os.cpu_count()}: cfg1 (N=1, 512x512, Lq=100) and bs={bs} 800x1333 encoder / "
-                   f"decoder layers, median of timed reps after warmups; value = {bs} images / (6 x (enc fwd + "
-                   f"enc fwd+bwd + dec fwd+bwd)) = {per_step(res[threads]):.2f} s of MSDA per step"),
+                   f"decoder layers, median of timed reps after warmups, at {sorted(res)} threads; value (best, "
+                   f"{best} threads) = {bs} images / (6 x ({'enc fwd + ' if recompute else ''}enc fwd+bwd + "
+                   f"dec fwd+bwd)) = {per_step(res[best]):.2f} s of MSDA per step"),
     }
 
 
@@ -287,6 +300,8 @@ def main(argv=None, device_type="cuda", child_script=None):
     args = make_args(device=str(device), backbone=a.backbone)
     model, criterion, _, optimizer = build_training(args, device)
     model.train(not a.forward_only)
+    from gdino_amd.train import set_activation_checkpointing
+    set_activation_checkpointing(model, a.checkpointing == "on")
     start_epoch = 0
     # reference main.py:339 (the cfg_odvg default: StepLR every lr_drop epochs)
     sched = torch.optim.lr_scheduler.StepLR(optimizer, args.lr_drop)
@@ -459,7 +474,10 @@ def main(argv=None, device_type="cuda", child_script=None):
             "config": {"workload": f"GroundingDINO-{a.backbone} + BERT-base {mode}, "
                                    f"{a.height}x{a.width}, 900 queries, 4 levels",
                        "global_batch": a.bs * world, "per_gpu_batch": a.bs, "image": [a.height, a.width],
-                       "text_tokens": 256, "parallelism": f"dp{world}"},
+                       "text_tokens": 256, "parallelism": f"dp{world}",
+                       "activation_checkpointing": a.checkpointing == "on",
+                       "peak_hbm_gb": (round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 1) if on_gpu
+                                       else None)},
             "roofline": roofline,
             "kernels": kernels,
             "hip_entry_points_one_step": hip_calls,
@@ -480,7 +498,7 @@ def main(argv=None, device_type="cuda", child_script=None):
         if not math.isfinite(loss_v):
             res["error"] = f"non-finite loss {loss_v}: the step diverged, the throughput is not a valid measurement"
         if not a.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(a.bs)
+            res["cpu_baseline"] = cpu_baseline(a.bs, recompute=a.checkpointing == "on")
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

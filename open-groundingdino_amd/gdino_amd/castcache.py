@@ -94,8 +94,15 @@ def _capturing(p: torch.Tensor) -> bool:
 
 
 SHADOWS = os.environ.get("GDINO_CAST_SHADOWS", "1") != "0"
-_shadow: dict = {}       # id(p) -> [weakref(p), bf16 shadow, p._version at the refresh]
+_shadow: dict = {}       # id(p) -> [weakref(p), bf16 shadow, p._version at the refresh, group key or None]
 _shadow_state = None     # (generation, dtype) of the last refresh
+# parameter groups the fused projections concatenate (_cached_cat): their
+# shadows are laid out back to back in one buffer, so the concatenation is
+# that buffer -- a view, no cat kernel per call (GDINO_GROUP_SHADOWS=0: off)
+GROUP_SHADOWS = os.environ.get("GDINO_GROUP_SHADOWS", "1") != "0"
+_groups: dict = {}       # key (tuple of ids) -> tuple of weakrefs, registered by _cached_cat
+_group_buf: dict = {}    # key -> the group's shadow buffer
+_groups_pending = False  # a group registered since the last layout
 
 
 class _ShadowCast(torch.autograd.Function):
@@ -134,21 +141,24 @@ def refresh_shadows(model: nn.Module, x: torch.Tensor) -> None:
     """Cast every trainable fp32 parameter of ``model`` into its persistent
     shadow in one multi-tensor copy, when a training forward under bf16
     autocast is about to run (x: any input on the model's device)."""
-    global _shadow_state
+    global _shadow_state, _groups_pending
     dt = autocast_dtype(x) if SHADOWS else None
     if dt is None or not torch.is_grad_enabled() or not model.training:
         return
     ps = _shadow_params(model)
     if not ps or any(q.device != x.device for q in ps):
         return
-    if _shadow_state == (_generation, dt) and not _capturing(x) and all(
+    if _shadow_state == (_generation, dt) and not _capturing(x) and not _groups_pending and all(
             _current_shadow(q, dt) is not None for q in ps):
         return  # already this step's weights (a second forward before the optimizer step)
+    if GROUP_SHADOWS:
+        _layout_groups(ps, dt)
+    _groups_pending = False
     dsts, srcs = [], []
     for q in ps:
         e = _shadow.get(id(q))
         if e is None or e[0]() is not q or e[1].shape != q.shape or e[1].dtype != dt:
-            e = [weakref.ref(q), torch.empty(q.shape, dtype=dt, device=q.device), None]
+            e = [weakref.ref(q), torch.empty(q.shape, dtype=dt, device=q.device), None, None]
             _shadow[id(q)] = e
         e[2] = q._version
         dsts.append(e[1])
@@ -156,6 +166,53 @@ def refresh_shadows(model: nn.Module, x: torch.Tensor) -> None:
     with torch.no_grad():
         torch._foreach_copy_(dsts, srcs)
     _shadow_state = (_generation, dt)
+
+
+def _layout_groups(ps, dt) -> None:
+    """Give every registered group whose members are all trainable shadowed
+    parameters one shadow buffer, the members' shadows being consecutive
+    slices of it along dim 0 (what torch.cat(dim=0) of them would produce).
+    A parameter takes part in one group at most; done once per group."""
+    live = {id(q) for q in ps}
+    taken = set()
+    for key, refs in list(_groups.items()):
+        members = [r() for r in refs]
+        if any(m is None for m in members):
+            del _groups[key]
+            _group_buf.pop(key, None)
+            continue
+        if not all(id(m) in live for m in members) or any(id(m) in taken for m in members):
+            continue
+        taken.update(id(m) for m in members)
+        buf = _group_buf.get(key)
+        tail = members[0].shape[1:]
+        if buf is not None and buf.dtype == dt and all(
+                (_shadow.get(id(m)) or [None] * 4)[3] == key for m in members):
+            continue  # laid out already
+        if any(m.shape[1:] != tail or m.device != members[0].device for m in members):
+            continue
+        buf = torch.empty((sum(m.shape[0] for m in members),) + tuple(tail), dtype=dt, device=members[0].device)
+        _group_buf[key] = buf
+        off = 0
+        for m in members:
+            n = m.shape[0]
+            _shadow[id(m)] = [weakref.ref(m), buf[off:off + n], None, key]
+            off += n
+
+
+class _GroupShadow(torch.autograd.Function):
+    """(p_1, ..., p_k) -> their group's shadow buffer (= the bf16 cat of the
+    parameters along dim 0); backward: split + ToCopyBackward per member."""
+
+    @staticmethod
+    def forward(ctx, buf, *ps):
+        ctx.rows = [p.shape[0] for p in ps]
+        ctx.dtypes = [p.dtype for p in ps]
+        return buf.detach()
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(x.to(d) for x, d in zip(g.split(ctx.rows, 0), ctx.dtypes))
 
 
 def _current_shadow(p: torch.Tensor, dtype: torch.dtype):
@@ -203,6 +260,8 @@ def clear() -> None:
     global _shadow_state
     _cache.clear()
     _shadow.clear()
+    _groups.clear()
+    _group_buf.clear()
     _shadow_state = None
 
 
@@ -281,8 +340,16 @@ def _cached_cat(params, dtype):
     """bf16 concatenation (dim 0) of several parameters, cached like
     cached_cast; gradients reach each parameter through the cat's split."""
     ps = tuple(params)
+    gkey = tuple(id(p) for p in ps)
+    if GROUP_SHADOWS and gkey not in _groups and all(p.requires_grad for p in ps):
+        global _groups_pending
+        _groups[gkey] = tuple(weakref.ref(p) for p in ps)  # laid out by the next refresh_shadows
+        _groups_pending = True
     shs = [_current_shadow(p, dtype) if p.requires_grad else None for p in ps]
     grad = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
+    if all(sh is not None for sh in shs) and all(_shadow[id(p)][3] == gkey for p in ps):
+        buf = _group_buf[gkey]
+        return _GroupShadow.apply(buf, *ps) if grad else buf  # the cat, as a buffer: no kernel
     if all(sh is not None for sh in shs):
         def make():  # one bf16 cat of the step's shadows (no fp32 cat + cast)
             return torch.cat([_from_shadow(p, sh, torch.is_grad_enabled()) for p, sh in zip(ps, shs)])

@@ -358,6 +358,29 @@ def forward_step(model, samples, captions, amp_dtype=torch.bfloat16):
         return model(samples, captions=captions)
 
 
+def set_activation_checkpointing(model, enabled: bool) -> int:
+    """Switch the reference's activation checkpointing (cfg use_checkpoint:
+    Swin blocks and fusion layers; use_transformer_ckpt: the deformable
+    encoder layers) on or off at run time.  It trades recompute for
+    activation memory: the backward re-runs each checkpointed forward.  The
+    losses and gradients are the same either way (the recompute replays the
+    RNG state; tests/test_model_cpu.py), so on a 288 GB MI355X, where the
+    bs=2 800x1333 step's activations fit many times over, the step can skip
+    the recompute.  Returns the number of modules switched."""
+    n = 0
+    for m in model.modules():
+        for attr in ("use_checkpoint", "use_transformer_ckpt"):
+            if isinstance(getattr(m, attr, None), bool):
+                setattr(m, attr, bool(enabled))
+                n += 1
+    return n
+
+
+def activation_checkpointing(model) -> bool:
+    return any(getattr(m, a, False) is True for m in model.modules()
+               for a in ("use_checkpoint", "use_transformer_ckpt"))
+
+
 def build_training(args, device):
     from models.GroundingDINO import build_groundingdino
     model, criterion, post = build_groundingdino(args)

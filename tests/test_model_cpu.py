@@ -343,3 +343,93 @@ def test_mixed_od_vg_batch_trains(built):
     with oracle_msda():
         loss = train_step(model, criterion, opt, samples, targets, caps, cats)
     assert torch.isfinite(loss)
+
+
+def test_activation_checkpointing_does_not_change_the_step():
+    """train.set_activation_checkpointing: the reference's checkpointing
+    (Swin blocks, fusion layers, encoder layers) only trades recompute for
+    memory -- with it off (the MI355X default: the activations stay in HBM)
+    the loss is bitwise the same and every gradient agrees to fp32 rounding
+    (summation order at the checkpoint boundaries), dropout / drop-path
+    included (the recompute replays the RNG state)."""
+    from gdino_amd.config import make_args
+    from gdino_amd.train import (activation_checkpointing, build_training, set_activation_checkpointing,
+                                 synthetic_batch, weighted_loss)
+    torch.manual_seed(0)
+    args = make_args(device="cpu", num_queries=60, enc_layers=2, dec_layers=2)
+    model, criterion, _, _ = build_training(args, "cpu")
+    model.train()
+    assert activation_checkpointing(model)  # cfg_odvg: use_checkpoint / use_transformer_ckpt
+    samples, targets, caps, cats = synthetic_batch(2, 96, 128, n_boxes=3, n_tokens=30, seed=3, device="cpu")
+    res = {}
+    for on in (True, False):
+        assert set_activation_checkpointing(model, on) > 0
+        model.zero_grad(set_to_none=True)
+        torch.manual_seed(123)
+        with oracle_msda():
+            out = model(samples, captions=caps)
+            loss = weighted_loss(criterion(out, targets, cats, caps), criterion.weight_dict)
+            loss.backward()
+        res[on] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert torch.equal(res[True][0], res[False][0])
+    assert set(res[True][1]) == set(res[False][1])
+    for n, g in res[True][1].items():
+        # a checkpoint boundary hands back its inputs' gradient contributions
+        # (the residual stream, the level / position embeddings used by every
+        # layer) in another summation order: fp32 rounding apart
+        r = res[False][1][n]
+        assert float((g - r).abs().max()) <= 1e-5 * float(r.abs().max().clamp_min(1e-30)), n
+    set_activation_checkpointing(model, True)
+
+
+def test_group_shadows_make_the_fused_projection_cat_a_view(built):
+    """castcache group shadows: the shadows of the parameters a fused
+    projection concatenates (MSDA offsets | weights, BiAttention v | values_v,
+    l | values_l) are laid out back to back, so the bf16 concatenation is a
+    buffer view instead of a cat kernel per call -- bitwise the same loss
+    and gradients as the cat path."""
+    from gdino_amd import castcache
+    from gdino_amd.train import synthetic_batch
+    args, model, criterion, *_ = built
+    samples, targets, caps, cats = synthetic_batch(2, 128, 160, n_boxes=3, n_tokens=40, seed=2, device="cpu")
+    model.train()
+    cat_calls = []
+
+    def run(group):
+        castcache.GROUP_SHADOWS = group
+        castcache.clear()
+        res = None
+        for it in range(2):  # the first forward registers the groups, the next refresh lays them out
+            torch.manual_seed(7)
+            for p in model.parameters():
+                p.grad = None
+            cat_calls.clear()
+            with oracle_msda(), torch.autocast("cpu", dtype=torch.bfloat16):
+                castcache._cache.clear()  # as under capture: no per-call cache, every fused call concatenates
+                orig_gs = castcache._GroupShadow.apply
+                castcache._GroupShadow.apply = lambda *a: cat_calls.append("view") or orig_gs(*a)
+                try:
+                    out = model(samples, captions=caps)
+                finally:
+                    castcache._GroupShadow.apply = orig_gs
+                ld = criterion(out, targets, cats, caps)
+                loss = sum(ld[k] * criterion.weight_dict[k] for k in ld if k in criterion.weight_dict)
+            with oracle_msda():  # the checkpoint recompute runs MSDA again
+                loss.backward()
+            res = (loss.detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                           if p.grad is not None}, cat_calls.count("view"),
+                   len(castcache._group_buf))
+        return res
+
+    try:
+        lc, gc, ncat_c, nb_c = run(False)
+        lg, gg, ncat_g, nb_g = run(True)
+    finally:
+        castcache.GROUP_SHADOWS = True
+        castcache.clear()
+    assert nb_c == 0 and nb_g >= 4
+    assert ncat_c == 0 and ncat_g >= 4  # the fused projections took the buffer views
+    assert torch.equal(lc, lg)
+    assert gc.keys() == gg.keys()
+    for n in gc:
+        assert torch.equal(gc[n], gg[n]), n
