@@ -270,11 +270,29 @@ class BiAttnTokens(torch.autograd.Function):
         return dqvv, dklv, None, None, None, None
 
 
+def _tunableop_tuning() -> bool:
+    t = getattr(torch.cuda, "tunable", None)
+    try:
+        return bool(t is not None and t.is_enabled() and t.tuning_is_enabled())
+    except (RuntimeError, AttributeError):
+        return False
+
+
 def tokens_ok(qvv, klv, nh) -> bool:
     """Token-major core applicable: ROCm device, one dtype (fp32 / bf16), the
     joint projection outputs [B, L, 2E] with unit channel stride and 16-B
     aligned rows, hd a multiple of 16 (bf16) / 64 (fp32)."""
     if qvv is None or klv is None:
+        return False
+    if _tunableop_tuning():
+        # PyTorch TunableOp, while TUNING, runs each candidate GEMM on copies
+        # of the operands sized max(stride * batch, m * k * batch) elements
+        # (GemmStridedBatchedParams::GetSizeA/B, ATen/cuda/tunable/
+        # GemmCommon.h): it assumes non-overlapping batches.  The per-head
+        # views below have batch stride hd = 256 < row stride 2E, so their
+        # true extent is ~2x that -- the candidates read past the copies
+        # (the round-3 hipErrorIllegalAddress of tools/tune_gemms.py).  While
+        # tuning, take the head-major path (contiguous per-head operands).
         return False
     ts = (qvv, klv)
     if not (all(_lib.on_device(t) for t in ts) and qvv.dtype == klv.dtype

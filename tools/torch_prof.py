@@ -28,11 +28,14 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=80)
+    ap.add_argument("--checkpointing", choices=("on", "off"), default="off")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     model, crit, _, opt = build_training(make_args(device="cuda"), dev)
     model.train()
+    from gdino_amd.train import set_activation_checkpointing
+    set_activation_checkpointing(model, a.checkpointing == "on")
     samples, targets, caps, cats = synthetic_batch(2, 800, 1333, n_boxes=8, n_tokens=256, seed=1000, device=dev)
     for _ in range(a.warmup):
         train_step(model, crit, opt, samples, targets, caps, cats)
