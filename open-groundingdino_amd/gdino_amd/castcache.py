@@ -256,6 +256,15 @@ def cached_cast(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return t
 
 
+def drop_autograd_refs() -> None:
+    """Forget the cached casts that carry a grad_fn: each keeps its
+    parameter's AccumulateGrad node (and the stream it was created on) alive
+    across steps.  The step-graph capture drops them so that every node of
+    the captured backward is (re)created on the capture stream."""
+    for k in [k for k, v in _cache.items() if v[3]]:
+        del _cache[k]
+
+
 def clear() -> None:
     global _shadow_state
     _cache.clear()

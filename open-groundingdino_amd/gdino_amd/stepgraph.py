@@ -118,22 +118,31 @@ class TrainStepGraph:
         for k, v in inputs.items():
             c.inputs[k] = _static_like(v)
         c.load(inputs)
+        # warm-up and capture on ONE side stream: the autograd engine runs a
+        # parameter's AccumulateGrad on the stream the node was created on
+        # (its first forward use); an AccumulateGrad node created on another
+        # stream and kept alive (e.g. by a cached weight cast's grad_fn) makes
+        # the captured backward synchronise with that stream, which HIP
+        # refuses during capture (hipErrorStreamCaptureUnsupported)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        castcache.drop_autograd_refs()
         with torch.cuda.stream(side):
             for _ in range(self.warmup):
                 if self.grad_sync is None:
                     self.optimizer.zero_grad(set_to_none=True)
                 self._body(c.inputs)
-        torch.cuda.current_stream().wait_stream(side)
+        castcache.drop_autograd_refs()
+        side.synchronize()
         if self.grad_sync is None:
             # the captured backward allocates the gradients from the graph's
             # pool; every replay rewrites them in place
             self.optimizer.zero_grad(set_to_none=True)
         # (a private memory pool per graph: a shared one would let a later
         # capture reuse memory an earlier graph's replays still write)
-        with torch.cuda.graph(c.graph):
+        with torch.cuda.graph(c.graph, stream=side):
             c.loss, c.loss_dict = self._body(c.inputs)
+        torch.cuda.current_stream().wait_stream(side)
         self.graphs[key] = c
         self.captures += 1
         return c
