@@ -15,6 +15,14 @@ def box_xyxy_to_cxcywh(x):
     return torch.stack(((x0 + x1) / 2, (y0 + y1) / 2, x1 - x0, y1 - y0), dim=-1)
 
 
+def _wh_area(wh):
+    """w * h of [..., 2] extents, as the reference's wh[..., 0] * wh[..., 1]
+    (util/box_ops.py) -- not a prod() reduction, whose backward checks the
+    input for zeros on the host (a device->host sync that HIP refuses inside
+    a graph capture: the whole-step graph's criterion backward)."""
+    return wh[..., 0] * wh[..., 1]
+
+
 def box_area(boxes):
     return (boxes[..., 2] - boxes[..., 0]) * (boxes[..., 3] - boxes[..., 1])
 
@@ -24,7 +32,7 @@ def box_iou(boxes1, boxes2):
     a1, a2 = box_area(boxes1), box_area(boxes2)
     lt = torch.maximum(boxes1[:, None, :2], boxes2[None, :, :2])
     rb = torch.minimum(boxes1[:, None, 2:], boxes2[None, :, 2:])
-    inter = (rb - lt).clamp(min=0).prod(-1)
+    inter = _wh_area((rb - lt).clamp(min=0))
     union = a1[:, None] + a2[None, :] - inter
     return inter / (union + 1e-6), union
 
@@ -34,7 +42,7 @@ def generalized_box_iou(boxes1, boxes2):
     iou, union = box_iou(boxes1, boxes2)
     lt = torch.minimum(boxes1[:, None, :2], boxes2[None, :, :2])
     rb = torch.maximum(boxes1[:, None, 2:], boxes2[None, :, 2:])
-    hull = (rb - lt).clamp(min=0).prod(-1)
+    hull = _wh_area((rb - lt).clamp(min=0))
     return iou - (hull - union) / (hull + 1e-6)
 
 
@@ -44,12 +52,12 @@ def paired_generalized_box_iou(boxes1, boxes2):
     a1, a2 = box_area(boxes1), box_area(boxes2)
     lt = torch.maximum(boxes1[:, :2], boxes2[:, :2])
     rb = torch.minimum(boxes1[:, 2:], boxes2[:, 2:])
-    inter = (rb - lt).clamp(min=0).prod(-1)
+    inter = _wh_area((rb - lt).clamp(min=0))
     union = a1 + a2 - inter
     iou = inter / (union + 1e-6)
     lt2 = torch.minimum(boxes1[:, :2], boxes2[:, :2])
     rb2 = torch.maximum(boxes1[:, 2:], boxes2[:, 2:])
-    hull = (rb2 - lt2).clamp(min=0).prod(-1)
+    hull = _wh_area((rb2 - lt2).clamp(min=0))
     return iou - (hull - union) / (hull + 1e-6)
 
 
@@ -59,8 +67,8 @@ def generalized_box_iou_batched(boxes1, boxes2):
     formula and epsilons as generalized_box_iou."""
     a1, a2 = box_area(boxes1), box_area(boxes2)
     b1, b2 = boxes1[..., :, None, :], boxes2[..., None, :, :]
-    inter = (torch.minimum(b1[..., 2:], b2[..., 2:]) - torch.maximum(b1[..., :2], b2[..., :2])).clamp(min=0).prod(-1)
+    inter = _wh_area((torch.minimum(b1[..., 2:], b2[..., 2:]) - torch.maximum(b1[..., :2], b2[..., :2])).clamp(min=0))
     union = a1[..., :, None] + a2[..., None, :] - inter
     iou = inter / (union + 1e-6)
-    hull = (torch.maximum(b1[..., 2:], b2[..., 2:]) - torch.minimum(b1[..., :2], b2[..., :2])).clamp(min=0).prod(-1)
+    hull = _wh_area((torch.maximum(b1[..., 2:], b2[..., 2:]) - torch.minimum(b1[..., :2], b2[..., :2])).clamp(min=0))
     return iou - (hull - union) / (hull + 1e-6)

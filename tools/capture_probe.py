@@ -12,6 +12,7 @@
 from __future__ import annotations
 
 import os
+import contextlib
 import sys
 import traceback
 
@@ -20,6 +21,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
 import torch  # noqa: E402
 from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
+
+
+NODE_LOG = []
 
 
 class OpLog(TorchDispatchMode):
@@ -103,9 +107,28 @@ def main():
 
         def body():
             ld, _ = crit.loss_prepared(out2, prep)
-            weighted_loss(ld, crit.weight_dict).backward()
+            loss = weighted_loss(ld, crit.weight_dict)
+            node_log = NODE_LOG
+            seen, stack = set(), [loss.grad_fn]
+            while stack:  # a pre-hook on every backward node: the last name printed ran last
+                n = stack.pop()
+                if n is None or n in seen:
+                    continue
+                seen.add(n)
+                n.register_prehook((lambda name: lambda *a: node_log.append(name))(n.name()))
+                stack.extend(f for f, _ in n.next_functions)
+            loss.backward()
         return body
 
+    if os.environ.get("PROBE_STEPGRAPH") == "1":
+        g2 = TrainStepGraph(model, crit, opt, warmup=2)
+        try:
+            g2(*b)
+            torch.cuda.synchronize()
+            print("CAPTURE TrainStepGraph: OK", flush=True)
+        except Exception as e:  # noqa: BLE001
+            print(f"CAPTURE TrainStepGraph: FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)
+        return
     pieces = [("criterion fwd+bwd", crit_only()),
               ("forward + loss", lambda: fwd_loss()),
               ("forward + loss + backward", lambda: fwd_loss()[0].backward()),
@@ -120,16 +143,17 @@ def main():
         torch.cuda.synchronize()
         opt.zero_grad(set_to_none=True)
         graph = torch.cuda.CUDAGraph()
-        oplog = OpLog()
+        oplog = OpLog() if os.environ.get("PROBE_OPLOG", "1") == "1" else contextlib.nullcontext()
         try:
-            with torch.cuda.graph(graph), oplog:
+            with torch.cuda.graph(graph, stream=s), oplog:
                 fn()
             graph.replay()
             torch.cuda.synchronize()
             print(f"CAPTURE {name}: OK", flush=True)
         except Exception as e:  # noqa: BLE001
             print(f"CAPTURE {name}: FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)
-            print(f"  last ops before the failure: {oplog.last[-8:]}", flush=True)
+            print(f"  last ops before the failure: {getattr(oplog, 'last', [])[-8:]}", flush=True)
+            print(f"  last backward nodes: {NODE_LOG[-6:]}", flush=True)
             traceback.print_exc(limit=6)
             break
 
