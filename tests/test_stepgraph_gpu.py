@@ -1,11 +1,12 @@
 """The whole train step as one HIP graph (gdino_amd.stepgraph.TrainStepGraph)
 against the eager train step (train.train_step) on the GPU: same model,
-weights and batches; after the same number of optimizer steps the losses
-and parameters agree (the only differences are float-atomic summation
-orders of the decoder MSDA backward and index_add, ~1e-7 relative).  Also:
-a second batch with other target counts replays the same graph (padded
-target slots), the LR scheduler acts on replays (lr is a device tensor),
-and the gradient all-reduce is captured (1-rank RCCL group)."""
+weights and batches, lr 0 so that every step sees the same weights; the
+losses and every parameter gradient agree (the only differences are
+float-atomic summation orders of the decoder MSDA backward and index_add).
+Also: a second batch with other target counts replays the same graph
+(padded target slots), the LR scheduler acts on replays (lr is a device
+tensor) and the captured AdamW moves the weights, and the gradient
+all-reduce is captured (1-rank RCCL group)."""
 import os
 import socket
 
@@ -40,46 +41,64 @@ def _params(model):
     return torch.cat([p.detach().reshape(-1).float() for p in model.parameters() if p.requires_grad])
 
 
+def _grads(model):
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
 def _run(grad_sync_factory=None):
+    """lr = 0 and no weight decay: the parameters stay put, so every eager
+    step and every replay sees the same weights and must give the same loss
+    and gradients (only float-atomic summation orders differ).  Then one
+    replay with lr > 0 must move the parameters (the captured AdamW step),
+    and the LR scheduler's value must reach the replay (lr is a device
+    tensor)."""
     from gdino_amd.stepgraph import TrainStepGraph
     from gdino_amd.train import train_step
     b1, b2 = _batch(11, 5), _batch(12, 3)
-    losses = {}
-    finals = {}
+    res = {}
     for mode in ("eager", "graph"):
         model, crit, opt = _model()
+        for g in opt.param_groups:
+            g["lr"], g["weight_decay"] = 0.0, 0.0
         sync = grad_sync_factory(model) if grad_sync_factory else None
-        sched = torch.optim.lr_scheduler.StepLR(opt, 1, gamma=0.5)
-        ls = []
+        out = []
         if mode == "eager":
-            for _ in range(3):  # = the graph's 2 warm-up steps + its first replay
-                ls.append(float(train_step(model, crit, opt, *b1, grad_sync=sync)))
-            sched.step()
-            ls.append(float(train_step(model, crit, opt, *b2, grad_sync=sync)))
+            for b in (b1, b2):
+                loss = float(train_step(model, crit, opt, *b, grad_sync=sync))
+                out.append((loss, _grads(model)))
         else:
             g = TrainStepGraph(model, crit, opt, grad_sync=sync, warmup=2)
-            ls.append(float(g(*b1)))
-            sched.step()  # fills the device lr tensors: acts on the replay
-            ls.append(float(g(*b2)))
+            for b in (b1, b2):
+                loss = float(g(*b))
+                out.append((loss, _grads(model)))
             assert g.captures == 1, "5 and 3 targets pad to the same 8-slot graph"
+            # the scheduler acts on the replays: a non-zero lr moves the weights
+            before = _params(model)
+            sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda e: 1.0)
+            for grp in opt.param_groups:
+                grp["initial_lr"] = 1e-4
+            sched.base_lrs = [1e-4] * len(opt.param_groups)
+            sched.step()
+            assert all(abs(float(grp["lr"]) - 1e-4) < 1e-9 for grp in opt.param_groups)
+            g(*b1)
+            torch.cuda.synchronize()
+            assert float((_params(model) - before).abs().max()) > 0
         torch.cuda.synchronize()
-        losses[mode] = ls
-        finals[mode] = _params(model)
-    return losses, finals
+        res[mode] = out
+    return res
 
 
-def _check(losses, finals):
-    le, lg = losses["eager"], losses["graph"]
-    assert abs(le[2] - lg[0]) <= 1e-4 * abs(le[2]), (le, lg)
-    assert abs(le[3] - lg[1]) <= 1e-4 * abs(le[3]), (le, lg)
-    d = (finals["eager"] - finals["graph"]).abs().max()
-    moved = (finals["eager"] - _params(_model()[0])).abs().max()
-    assert moved > 0
-    assert float(d) <= 1e-3 * float(moved), (float(d), float(moved))
+def _check(res):
+    for (le, ge), (lg, gg) in zip(res["eager"], res["graph"]):
+        assert abs(le - lg) <= 1e-5 * abs(le), (le, lg)
+        assert ge.keys() == gg.keys() and len(ge) > 100
+        for n in ge:
+            d = float((ge[n] - gg[n]).norm() / ge[n].norm().clamp_min(1e-30))
+            assert d <= 1e-3, (n, d)
 
 
 def test_step_graph_matches_eager_steps():
-    _check(*_run())
+    _check(_run())
 
 
 def _free_port():
@@ -100,7 +119,7 @@ def test_step_graph_captures_the_bucketed_allreduce():
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
     try:
-        losses, finals = _run(lambda m: BucketedGradSync(m.parameters(), bucket_mb=4, first_bucket_mb=1))
+        res = _run(lambda m: BucketedGradSync(m.parameters(), bucket_mb=4, first_bucket_mb=1))
     finally:
         dist.destroy_process_group()
-    _check(losses, finals)
+    _check(res)
