@@ -91,6 +91,98 @@ contrastive_kernel(const T* __restrict__ x, int64_t xsb, int64_t xsq, const T* _
     }
 }
 
+// v2 (round 4): the round-3 kernel gave a wave 64 rows x every token, so
+// the decoder call (B = 2, Q = 900) ran 32 waves on a 1024-SIMD chip and
+// each wave walked 8 dependent load -> MFMA rounds per token tile: 47 us of
+// latency for 2.7 MB.  Here a workgroup owns 16 * QT rows and its 4 waves
+// split the token tiles (wave w: tokens 64w .. 64w + 63, then + 256 ...), so
+// the decoder call is 456 waves (QT = 1) and the encoder's row-max call 2 784
+// (QT = 4); the next K chunk's operands are loaded while the current
+// chunk's MFMAs run, and the row maxima of the 4 waves meet in LDS.
+template <typename T, int QT>
+__global__ void __launch_bounds__(256)
+contrastive_v2_kernel(const T* __restrict__ x, int64_t xsb, int64_t xsq, const T* __restrict__ text, int64_t tsb,
+                      int64_t tst, const uint8_t* __restrict__ tmask, int Q, int Tn, int C, int Tout,
+                      float* __restrict__ out, float* __restrict__ rowmax) {
+  __shared__ float smax[4][16 * QT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y;
+  const int q0 = blockIdx.x * 16 * QT;
+  const T* xb = x + b * xsb;
+  const T* tb = text + b * tsb;
+  float mx[QT][4];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[qt][r] = -INFINITY;
+  const int nch = C / 32;
+  for (int t0 = 64 * wave; t0 < Tout; t0 += 256) {
+    gd_f32x4 acc[QT][4];  // (row q0 + 16qt + 4g + r, token t0 + 16tt + c)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) acc[qt][tt] = zero4();
+    if (t0 < Tn) {
+      auto load = [&](int ch, WFrag<T>* tf, WFrag<T>* xf) {
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const int t = t0 + 16 * tt + c;
+          tf[tt] = ld_frag<T>(tb + int64_t(t < Tn ? t : 0) * tst + 32 * ch + 8 * g, t < Tn);
+        }
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          const int q = q0 + 16 * qt + c;
+          xf[qt] = ld_frag<T>(xb + int64_t(q < Q ? q : 0) * xsq + 32 * ch + 8 * g, q < Q);
+        }
+      };
+      WFrag<T> tf[2][4], xf[2][QT];
+      load(0, tf[0], xf[0]);
+      for (int ch = 0; ch < nch; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < nch) load(ch + 1, tf[cur ^ 1], xf[cur ^ 1]);  // next chunk in flight
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) acc[qt][tt] = wmma(xf[cur][qt], tf[cur][tt], acc[qt][tt]);
+      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int t = t0 + 16 * tt + c;
+      const bool live = t < Tn && tmask[int64_t(b) * Tn + t] != 0;
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = q0 + 16 * qt + 4 * g + r;
+          const float v = live ? acc[qt][tt][r] : -INFINITY;
+          mx[qt][r] = fmaxf(mx[qt][r], v);
+          if (out && q < Q && t < Tout) out[(int64_t(b) * Q + q) * Tout + t] = v;
+        }
+    }
+  }
+  if (!rowmax) return;  // uniform over the workgroup: no barrier skipped by part of it
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float m = mx[qt][r];
+      m = fmaxf(m, __shfl_xor(m, 1, 64));
+      m = fmaxf(m, __shfl_xor(m, 2, 64));
+      m = fmaxf(m, __shfl_xor(m, 4, 64));
+      m = fmaxf(m, __shfl_xor(m, 8, 64));
+      if (c == 0) smax[wave][16 * qt + 4 * g + r] = m;
+    }
+  __syncthreads();
+  if (threadIdx.x < 16 * QT) {
+    const int q = q0 + threadIdx.x;
+    const float m = fmaxf(fmaxf(smax[0][threadIdx.x], smax[1][threadIdx.x]),
+                          fmaxf(smax[2][threadIdx.x], smax[3][threadIdx.x]));
+    if (q < Q) rowmax[int64_t(b) * Q + q] = m;
+  }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
@@ -113,16 +205,40 @@ extern "C" gd_status gd_contrastive_forward(gd_dtype dt, const void* x, const in
                  text_strides[0] % align == 0 && text_strides[1] % align == 0,
              "contrastive: x / text rows must be contiguous and 16-byte aligned");
   hipStream_t s = as_hip(stream);
-  const dim3 grid(unsigned((Q + 255) / 256), unsigned(B));
-  if (dt == GD_BF16) {
-    hipLaunchKernelGGL((contrastive_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)x, x_strides[0],
-                       x_strides[1], (const uint16_t*)text, text_strides[0], text_strides[1], text_mask, Q, T, C,
-                       Tout, logits, rowmax);
-  } else {
-    hipLaunchKernelGGL((contrastive_kernel<float>), grid, dim3(256), 0, s, (const float*)x, x_strides[0],
-                       x_strides[1], (const float*)text, text_strides[0], text_strides[1], text_mask, Q, T, C, Tout,
-                       logits, rowmax);
+  // GD_CONTRASTIVE_V=1: the round-3 kernel (64 rows x all tokens per wave), A/B
+  if (env_int("GD_CONTRASTIVE_V", 2) == 1) {
+    const dim3 grid(unsigned((Q + 255) / 256), unsigned(B));
+    if (dt == GD_BF16) {
+      hipLaunchKernelGGL((contrastive_kernel<uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)x, x_strides[0],
+                         x_strides[1], (const uint16_t*)text, text_strides[0], text_strides[1], text_mask, Q, T, C,
+                         Tout, logits, rowmax);
+    } else {
+      hipLaunchKernelGGL((contrastive_kernel<float>), grid, dim3(256), 0, s, (const float*)x, x_strides[0],
+                         x_strides[1], (const float*)text, text_strides[0], text_strides[1], text_mask, Q, T, C,
+                         Tout, logits, rowmax);
+    }
+    GD_LAUNCH_CHECK("contrastive");
+    return GD_OK;
   }
-  GD_LAUNCH_CHECK("contrastive");
+  // 4 row tiles per workgroup when that still leaves >= 2 workgroups per CU
+  const bool wide = int64_t(B) * ((Q + 63) / 64) >= 512;
+  const int rows = wide ? 64 : 16;
+  const dim3 grid(unsigned((Q + rows - 1) / rows), unsigned(B));
+  auto launch = [&](auto tag) {
+    using E = decltype(tag);
+    const E* xp = static_cast<const E*>(x);
+    const E* tp = static_cast<const E*>(text);
+    if (wide)
+      hipLaunchKernelGGL((contrastive_v2_kernel<E, 4>), grid, dim3(256), 0, s, xp, x_strides[0], x_strides[1], tp,
+                         text_strides[0], text_strides[1], text_mask, Q, T, C, Tout, logits, rowmax);
+    else
+      hipLaunchKernelGGL((contrastive_v2_kernel<E, 1>), grid, dim3(256), 0, s, xp, x_strides[0], x_strides[1], tp,
+                         text_strides[0], text_strides[1], text_mask, Q, T, C, Tout, logits, rowmax);
+  };
+  if (dt == GD_BF16)
+    launch(uint16_t{});
+  else
+    launch(float{});
+  GD_LAUNCH_CHECK("contrastive_v2");
   return GD_OK;
 }

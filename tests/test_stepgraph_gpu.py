@@ -56,13 +56,13 @@ def _run(grad_sync_factory=None):
     from gdino_amd.train import train_step
     b1, b2 = _batch(11, 5), _batch(12, 3)
     res = {}
-    for mode in ("eager", "graph"):
+    for mode in ("eager", "eager2", "graph"):
         model, crit, opt = _model()
         for g in opt.param_groups:
             g["lr"], g["weight_decay"] = 0.0, 0.0
         sync = grad_sync_factory(model) if grad_sync_factory else None
         out = []
-        if mode == "eager":
+        if mode.startswith("eager"):
             for b in (b1, b2):
                 loss = float(train_step(model, crit, opt, *b, grad_sync=sync))
                 out.append((loss, _grads(model)))
@@ -89,12 +89,17 @@ def _run(grad_sync_factory=None):
 
 
 def _check(res):
-    for (le, ge), (lg, gg) in zip(res["eager"], res["graph"]):
-        assert abs(le - lg) <= 1e-5 * abs(le), (le, lg)
+    """graph vs eager within max(1e-3, 3x the eager run-to-run spread): the
+    float atomics (decoder MSDA backward into an fp32 buffer later rounded
+    to bf16, index_add) change summation orders between any two runs"""
+    def rel(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+    for (le, ge), (le2, ge2), (lg, gg) in zip(res["eager"], res["eager2"], res["graph"]):
+        assert abs(le - lg) <= max(1e-5 * abs(le), 3 * abs(le - le2)), (le, le2, lg)
         assert ge.keys() == gg.keys() and len(ge) > 100
         for n in ge:
-            d = float((ge[n] - gg[n]).norm() / ge[n].norm().clamp_min(1e-30))
-            assert d <= 1e-3, (n, d)
+            d, noise = rel(gg[n], ge[n]), rel(ge2[n], ge[n])
+            assert d <= max(1e-3, 3 * noise), (n, d, noise)
 
 
 def test_step_graph_matches_eager_steps():
