@@ -221,7 +221,9 @@ extern "C" gd_status gd_contrastive_forward(gd_dtype dt, const void* x, const in
     return GD_OK;
   }
   // 4 row tiles per workgroup when that still leaves >= 2 workgroups per CU
-  const bool wide = int64_t(B) * ((Q + 63) / 64) >= 512;
+  // (GD_CONTRASTIVE_WIDE=0 / 1 forces the 16- / 64-row workgroups: tests)
+  const int wide_env = env_int("GD_CONTRASTIVE_WIDE", -1);
+  const bool wide = wide_env >= 0 ? wide_env == 1 : int64_t(B) * ((Q + 63) / 64) >= 512;
   const int rows = wide ? 64 : 16;
   const dim3 grid(unsigned((Q + rows - 1) / rows), unsigned(B));
   auto launch = [&](auto tag) {

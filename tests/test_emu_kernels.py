@@ -716,8 +716,12 @@ def test_emulated_attention_dropout(dtype, tol):
     (1, 70, 256, 256, 256, torch.float32, 1e-5),   # full caption, hidden 256
     (2, 130, 90, 256, 256, torch.bfloat16, 1e-5),  # bf16-exact inputs, fp32 accumulation
 ])
-def test_emulated_contrastive(B, Q, T, C, tout, dtype, tol):
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_emulated_contrastive(B, Q, T, C, tout, dtype, tol, wide, monkeypatch):
+    """both workgroup shapes of the v2 kernel (16 rows, 64 rows per
+    workgroup; GD_CONTRASTIVE_WIDE forces one)"""
     from oracle.blocks import contrastive_ref
+    monkeypatch.setenv("GD_CONTRASTIVE_WIDE", wide)
     g = torch.Generator().manual_seed(Q + T)
     x = torch.randn(B, Q, C, generator=g).to(dtype)
     text = torch.randn(B, T, C, generator=g).to(dtype)
