@@ -114,17 +114,36 @@ def _free_port():
     return port
 
 
+def _allreduce_child():
+    """Runs in a child process (the RCCL communicator's lifetime is the
+    process's, and a captured graph holding its collectives must be freed
+    before the process group is destroyed)."""
+    import gc
+    import torch.distributed as dist
+    from gdino_amd.train import BucketedGradSync
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
+    try:
+        res = _run(lambda m: BucketedGradSync(m.parameters(), bucket_mb=4, first_bucket_mb=1))
+        _check(res)
+    finally:
+        gc.collect()
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+    print("ALLREDUCE_CAPTURE_OK", flush=True)
+
+
 def test_step_graph_captures_the_bucketed_allreduce():
     """BucketedGradSync inside the captured step on a 1-rank RCCL group: the
     per-bucket all-reduces are graph nodes (a 1-rank sum is the identity, so
     the result must equal the eager steps)."""
-    import torch.distributed as dist
-    from gdino_amd.train import BucketedGradSync
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
-    try:
-        res = _run(lambda m: BucketedGradSync(m.parameters(), bucket_mb=4, first_bucket_mb=1))
-    finally:
-        dist.destroy_process_group()
-    _check(res)
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_stepgraph_gpu as t; t._allreduce_child()"
+            % (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "open-groundingdino_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ALLREDUCE_CAPTURE_OK" in r.stdout, (r.returncode, r.stdout[-2000:],
+                                                                      r.stderr[-4000:])
