@@ -501,6 +501,15 @@ def main(argv=None, device_type="cuda", child_script=None):
             res["cpu_baseline"] = cpu_baseline(a.bs, recompute=a.checkpointing == "on")
         print(json.dumps(res), flush=True)
     if world > 1:
+        # the captured step holds RCCL collectives: free it before the
+        # communicator goes (destroying a process group under a live graph
+        # that references it aborts)
+        if step_graph is not None:
+            step_graph.release()
+        step = None
+        import gc
+        gc.collect()
+        sync()
         dist.destroy_process_group()
     if not math.isfinite(loss_v):
         raise SystemExit(1)
