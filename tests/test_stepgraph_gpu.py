@@ -19,10 +19,11 @@ DEV = "cuda"
 
 def _model(seed=0):
     from gdino_amd.config import make_args
-    from gdino_amd.train import build_training
+    from gdino_amd.train import build_training, set_activation_checkpointing
     torch.manual_seed(seed)
     args = make_args(device=DEV, enc_layers=2, dec_layers=2, num_queries=300)
     model, criterion, _, opt = build_training(args, torch.device(DEV))
+    set_activation_checkpointing(model, CKPT[0])
     for m in model.modules():  # the same function in both runs (dropout draws differ)
         if isinstance(m, torch.nn.Dropout):
             m.p = 0.0
@@ -102,8 +103,18 @@ def _check(res):
             assert d <= max(1e-3, 3 * noise), (n, d, noise)
 
 
-def test_step_graph_matches_eager_steps():
-    _check(_run())
+CKPT = [True]
+
+
+@pytest.mark.parametrize("ckpt", [True, False])
+def test_step_graph_matches_eager_steps(ckpt):
+    """with and without the reference's activation checkpointing (the bench
+    default is without)"""
+    CKPT[0] = ckpt
+    try:
+        _check(_run())
+    finally:
+        CKPT[0] = True
 
 
 def _free_port():

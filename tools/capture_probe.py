@@ -47,12 +47,15 @@ def main():
         weighted_loss
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    args = make_args(device="cuda", enc_layers=2, dec_layers=2, num_queries=300)
+    full = os.environ.get("PROBE_FULL") == "1"  # the bench's shapes
+    args = make_args(device="cuda") if full else make_args(device="cuda", enc_layers=2, dec_layers=2,
+                                                           num_queries=300)
     model, crit, _, opt = build_training(args, dev)
     model.train()
     ckpt = os.environ.get("PROBE_CKPT", "off") == "on"
     set_activation_checkpointing(model, ckpt)
-    b = synthetic_batch(2, 320, 384, n_boxes=5, n_tokens=40, seed=11, device=dev)
+    b = (synthetic_batch(2, 800, 1333, n_boxes=8, n_tokens=256, seed=1000, device=dev) if full else
+         synthetic_batch(2, 320, 384, n_boxes=5, n_tokens=40, seed=11, device=dev))
     train_step(model, crit, opt, *b)
     torch.cuda.synchronize()
     print(f"checkpointing={ckpt}; eager step under sync debug mode:", flush=True)
@@ -147,8 +150,11 @@ def main():
         try:
             with torch.cuda.graph(graph, stream=s), oplog:
                 fn()
-            graph.replay()
-            torch.cuda.synchronize()
+            print(f"CAPTURE {name}: captured, replaying", flush=True)
+            for i in range(int(os.environ.get("PROBE_REPLAYS", "1"))):
+                graph.replay()
+                torch.cuda.synchronize()
+                print(f"  replay {i} done", flush=True)
             print(f"CAPTURE {name}: OK", flush=True)
         except Exception as e:  # noqa: BLE001
             print(f"CAPTURE {name}: FAILED {type(e).__name__}: {str(e)[:200]}", flush=True)
