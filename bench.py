@@ -112,12 +112,16 @@ def launch_ranks(n, argv, script=None):
     return subprocess.call(cmd, env=env)
 
 
-def setup_dist(n, on_gpu=True):
+def setup_dist(n, on_gpu=True, capture=False):
     if n <= 1 and "RANK" not in os.environ:
         return 0, 1, 0
     local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
     if on_gpu:
         torch.cuda.set_device(local)  # bind the device before RCCL creates its communicator
+        if capture:  # collectives inside the step graph (gdino_amd.stepgraph.RCCL_CAPTURE_ENV)
+            from gdino_amd.stepgraph import RCCL_CAPTURE_ENV
+            for k, v in RCCL_CAPTURE_ENV.items():
+                os.environ.setdefault(k, v)
     dist.init_process_group("nccl" if on_gpu else "gloo")  # gloo: CPU contract test only
     return dist.get_rank(), dist.get_world_size(), local
 
@@ -284,7 +288,8 @@ def main(argv=None, device_type="cuda", child_script=None):
             raise SystemExit(rc)
         return
     on_gpu = device_type == "cuda"
-    rank, world, local = setup_dist(a.gpus, on_gpu)
+    rank, world, local = setup_dist(a.gpus, on_gpu,
+                                    capture=(a.graphs is not False) and on_gpu and not a.forward_only)
     device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     if on_gpu:

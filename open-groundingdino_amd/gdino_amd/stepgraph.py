@@ -33,6 +33,18 @@ from . import castcache
 from .train import BucketedGradSync, weighted_loss
 
 
+# Process-group settings for collectives inside a captured graph, to be in
+# the environment before init_process_group (bench.setup_dist sets them when
+# the step graph runs with N > 1):
+#  * no CUDA-event cache: ProcessGroupNCCL recycles its work events, and its
+#    watchdog thread querying an event whose last record was made inside a
+#    capture fails with hipErrorCapturedEvent and terminates the process
+#    (seen on a 1-rank RCCL group, tests/test_stepgraph_gpu.py);
+#  * no async error handling (the watchdog's abort path), as PyTorch's CUDA
+#    graph notes prescribe for captured collectives.
+RCCL_CAPTURE_ENV = {"TORCH_NCCL_CUDA_EVENT_CACHE": "0", "TORCH_NCCL_ASYNC_ERROR_HANDLING": "0"}
+
+
 def _static_like(t: torch.Tensor) -> torch.Tensor:
     return torch.empty_like(t, memory_format=torch.contiguous_format)
 

@@ -144,6 +144,11 @@ def _allreduce_child():
     print("ALLREDUCE_CAPTURE_OK", flush=True)
 
 
+def train_capture_env():
+    from gdino_amd.stepgraph import RCCL_CAPTURE_ENV
+    return dict(RCCL_CAPTURE_ENV)
+
+
 def test_step_graph_captures_the_bucketed_allreduce():
     """BucketedGradSync inside the captured step on a 1-rank RCCL group: the
     per-bucket all-reduces are graph nodes (a 1-rank sum is the identity, so
@@ -152,6 +157,7 @@ def test_step_graph_captures_the_bucketed_allreduce():
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    env.update(train_capture_env())
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_stepgraph_gpu as t; t._allreduce_child()"
             % (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "open-groundingdino_amd")))
