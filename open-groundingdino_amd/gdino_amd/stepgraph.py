@@ -146,6 +146,15 @@ class TrainStepGraph:
                 self._body(c.inputs)
         castcache.drop_autograd_refs()
         side.synchronize()
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            # ProcessGroupNCCL's watchdog thread polls the warm-up's
+            # collectives (about every 100 ms) by querying their end events,
+            # recorded on the communication stream; once the capture forks
+            # that stream, HIP refuses the query (hipErrorCapturedEvent) and
+            # the watchdog terminates the process.  Let it retire them first.
+            import time
+            torch.cuda.synchronize()
+            time.sleep(1.0)
         if self.grad_sync is None:
             # the captured backward allocates the gradients from the graph's
             # pool; every replay rewrites them in place
