@@ -29,8 +29,19 @@ from __future__ import annotations
 
 import torch
 
+import os
+import sys
+import time
+
 from . import castcache
 from .train import BucketedGradSync, weighted_loss
+
+_VERBOSE = os.environ.get("GDINO_STEPGRAPH_VERBOSE") == "1"
+
+
+def _log(msg):
+    if _VERBOSE:
+        print(f"[stepgraph {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 # Process-group settings for collectives inside a captured graph, to be in
@@ -140,10 +151,13 @@ class TrainStepGraph:
         side.wait_stream(torch.cuda.current_stream())
         castcache.drop_autograd_refs()
         with torch.cuda.stream(side):
-            for _ in range(self.warmup):
+            for i in range(self.warmup):
                 if self.grad_sync is None:
                     self.optimizer.zero_grad(set_to_none=True)
                 self._body(c.inputs)
+                if _VERBOSE:
+                    side.synchronize()
+                    _log(f"warm-up step {i} done")
         castcache.drop_autograd_refs()
         side.synchronize()
         if torch.distributed.is_available() and torch.distributed.is_initialized():
@@ -161,9 +175,11 @@ class TrainStepGraph:
             self.optimizer.zero_grad(set_to_none=True)
         # (a private memory pool per graph: a shared one would let a later
         # capture reuse memory an earlier graph's replays still write)
+        _log("capture begins")
         with torch.cuda.graph(c.graph, stream=side):
             c.loss, c.loss_dict = self._body(c.inputs)
         torch.cuda.current_stream().wait_stream(side)
+        _log(f"captured ({c.graph.__class__.__name__})")
         self.graphs[key] = c
         self.captures += 1
         return c
@@ -178,6 +194,9 @@ class TrainStepGraph:
             c.load(inputs)
         c.graph.replay()
         castcache._on_optimizer_step()  # the replay stepped the optimizer: cast copies are stale
+        if _VERBOSE:
+            torch.cuda.synchronize()
+            _log(f"replay done, loss {float(c.loss):.4f}")
         return c.loss
 
     def release(self):
