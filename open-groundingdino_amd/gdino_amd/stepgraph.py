@@ -88,6 +88,11 @@ class TrainStepGraph:
         self.grad_sync, self.warmup, self.kmax_multiple = grad_sync, warmup, kmax_multiple
         self.graphs = {}
         self.captures = 0
+        # replays in flight on the device at most (the host prepares the next
+        # step's inputs meanwhile); back-to-back launches of this ~5 000-node
+        # graph with no bound hung the GPU twice on the box
+        self.max_inflight = max(1, int(os.environ.get("GDINO_STEPGRAPH_INFLIGHT", "1")))
+        self._inflight = []
         device = next(model.parameters()).device
         for g in optimizer.param_groups:  # capturable fused AdamW; lr a device tensor the scheduler fills
             g["capturable"] = True
@@ -185,6 +190,10 @@ class TrainStepGraph:
         return c
 
     def __call__(self, samples, targets, captions, cat_lists):
+        # the previous replay finishes before this step enqueues anything
+        # (its input copies included): see max_inflight
+        while len(self._inflight) >= self.max_inflight:
+            self._inflight.pop(0).synchronize()
         inputs = self._prepare(samples, targets, captions, cat_lists)
         key = self._signature(inputs)
         c = self.graphs.get(key)
@@ -193,6 +202,9 @@ class TrainStepGraph:
         else:
             c.load(inputs)
         c.graph.replay()
+        ev = torch.cuda.Event()
+        ev.record()
+        self._inflight.append(ev)
         castcache._on_optimizer_step()  # the replay stepped the optimizer: cast copies are stale
         if _VERBOSE:
             torch.cuda.synchronize()
@@ -200,4 +212,7 @@ class TrainStepGraph:
         return c.loss
 
     def release(self):
+        for ev in self._inflight:
+            ev.synchronize()
+        self._inflight.clear()
         self.graphs.clear()
