@@ -68,15 +68,27 @@ def prepare_text_host(tokenizer, special_tokens, max_text_len, captions):
     return text, tokenized
 
 
+_STAGING = []  # (pinned host buffer, event recorded after its copy)
+
+
 def to_device_async(t: torch.Tensor, device) -> torch.Tensor:
     """Host tensor -> device without a stream synchronisation: a pageable
     source copied with non_blocking=False makes torch wait for the whole
     stream (the queued forward included) before the copy; staging it through
-    pinned memory (torch's caching host allocator) keeps the copy async."""
+    pinned memory keeps the copy async.  The staging buffer is held here
+    until an event recorded after the copy has completed, so it cannot be
+    reused while the copy still waits in the stream behind queued work."""
     device = torch.device(device)
     if device.type != "cuda" or t.device.type != "cpu":
         return t.to(device)
-    return (t if t.is_pinned() else t.pin_memory()).to(device, non_blocking=True)
+    while _STAGING and _STAGING[0][1].query():
+        _STAGING.pop(0)
+    pinned = t if t.is_pinned() else t.pin_memory()
+    out = pinned.to(device, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _STAGING.append((pinned, ev))
+    return out
 
 
 class GroundingDINO(nn.Module):
