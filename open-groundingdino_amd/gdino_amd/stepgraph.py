@@ -88,10 +88,16 @@ class TrainStepGraph:
         self.grad_sync, self.warmup, self.kmax_multiple = grad_sync, warmup, kmax_multiple
         self.graphs = {}
         self.captures = 0
-        # replays in flight on the device at most (the host prepares the next
-        # step's inputs meanwhile); back-to-back launches of this ~5 000-node
-        # graph with no bound hung the GPU twice on the box
-        self.max_inflight = max(1, int(os.environ.get("GDINO_STEPGRAPH_INFLIGHT", "1")))
+        # After each replay the host waits for the whole device
+        # (hipDeviceSynchronize) before it enqueues the next step's input
+        # copies: with the next step's copies and replay enqueued behind a
+        # running replay -- unbounded, or bounded by an event recorded after
+        # the launch -- the box faulted (illegal address) within the first
+        # replays; with a device-wide sync after every replay it ran clean
+        # (DESIGN §7).  The host's preparation of a step (~2 ms) is then not
+        # hidden.  GDINO_STEPGRAPH_SYNC=event: the event-bounded variant.
+        self.sync_mode = os.environ.get("GDINO_STEPGRAPH_SYNC", "device")
+        self.max_inflight = 1
         self._inflight = []
         device = next(model.parameters()).device
         for g in optimizer.param_groups:  # capturable fused AdamW; lr a device tensor the scheduler fills
@@ -202,9 +208,12 @@ class TrainStepGraph:
         else:
             c.load(inputs)
         c.graph.replay()
-        ev = torch.cuda.Event()
-        ev.record()
-        self._inflight.append(ev)
+        if self.sync_mode == "device":
+            torch.cuda.synchronize()
+        else:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._inflight.append(ev)
         castcache._on_optimizer_step()  # the replay stepped the optimizer: cast copies are stale
         if _VERBOSE:
             torch.cuda.synchronize()
