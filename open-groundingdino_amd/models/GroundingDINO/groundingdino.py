@@ -475,8 +475,8 @@ class SetCriterion(nn.Module):
         rows, cols = lsap.linear_sum_assignment_batched(cost.reshape(H * B, Q, K), sizes.repeat(H))
         w = (rows >= 0).view(-1)                                            # [H*B*K] real pairs
         hi, bi = self._pair_heads(H, B, K, device)
-        qi = rows.clamp(min=0).view(-1)
-        ki = cols.clamp(min=0).view(-1)
+        qi = rows.clamp(0, Q - 1).view(-1)  # (the solver writes every slot; the clamps keep any index in range)
+        ki = cols.clamp(0, K - 1).view(-1)
         npos = torch.clamp(torch.minimum(sizes, torch.full_like(sizes, Q)).sum().float(), min=1.0)
 
         # token-level sigmoid focal loss (token_sigmoid_binary_focal_loss, :462-496); padded
