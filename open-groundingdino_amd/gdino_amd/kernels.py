@@ -163,3 +163,4 @@ from . import contrastive  # noqa: E402,F401
 from . import msda_prologue  # noqa: E402,F401
 from . import wgrad  # noqa: E402,F401
 from . import layernorm  # noqa: E402,F401
+from . import lsap  # noqa: E402,F401  (the device Hungarian matching)
