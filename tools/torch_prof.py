@@ -59,15 +59,30 @@ def main():
     import collections
     agg = collections.Counter()
     cnt = collections.Counter()
+    def site(e):
+        """innermost product frame (forward ops), else the autograd node whose
+        backward issued the op (backward ops run on the engine's thread
+        without a Python stack), else the nearest named parent range"""
+        frame = next((f for f in (e.stack or []) if "open-groundingdino_amd" in f or "bench.py" in f), "")
+        if frame:
+            return frame.split("open-groundingdino_amd/")[-1]
+        p = e.cpu_parent
+        while p is not None:
+            if p.name.startswith("autograd::engine::evaluate_function: "):
+                return "bwd " + p.name.split(": ", 1)[1]
+            p = p.cpu_parent
+        p = e.cpu_parent
+        while p is not None and p.name.startswith("aten::"):
+            p = p.cpu_parent
+        return ("in " + p.name) if p is not None else ""
+
     for e in prof.events():
         t = getattr(e, "self_device_time_total", None)
         if t is None:
             t = e.self_cuda_time_total
         if not t or not e.name.startswith("aten::"):
             continue
-        frame = next((f for f in (e.stack or []) if "open-groundingdino_amd" in f or "bench.py" in f), "")
-        frame = frame.split("open-groundingdino_amd/")[-1]
-        k = (e.name, str(e.input_shapes)[:110], frame[:90])
+        k = (e.name, str(e.input_shapes)[:110], site(e)[:90])
         agg[k] += t
         cnt[k] += 1
     tot = sum(agg.values())
