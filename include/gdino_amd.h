@@ -65,6 +65,12 @@
  *                        deformable encoder / decoder layers and the text
  *                        enhancer (transformer.py:789-808, 877-936,
  *                        transformer_vanilla.py:83-110) and its backward
+ *   gd_add_scaled_forward / _backward / _workspace_bytes
+ *                     <- the layer-scale / drop-path residual endings
+ *                        `v = v + drop_path(gamma_v * delta_v)` of the
+ *                        BiAttention fusion block (fuse_modules.py:285-286)
+ *                        and `x = shortcut + drop_path(x)` of the Swin blocks
+ *                        (swin_transformer.py:295-296) and their backward
  *   gd_contrastive_forward
  *                     <- ContrastiveEmbed.forward (x . text^T, -inf on padded
  *                        tokens, -inf right padding to max_text_len)
@@ -391,6 +397,29 @@ gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_
                                     const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,
                                     float* grad_weight, float* grad_bias, void* workspace,
                                     gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Scaled residual ending (fuse_modules.py:285-286, swin_transformer.py:295-296) */
+/* ------------------------------------------------------------------------ */
+/*
+ * x, branch, out [B, N, C] contiguous (F32 or BF16 each, vector aligned:
+ * 16 B for F32, 8 B for BF16), C % 4 == 0, C <= 1024; s F32 with
+ * s[b][c] at s + b * s_bstride + c * s_cstride (s_cstride 0 or 1; strides 0
+ * broadcast).  out = x + branch * s in fp32, rounded to out's dtype.
+ * Backward: grad_out (F32 or BF16) -> grad_branch = grad_out * s in
+ * branch's dtype (or NULL) and grad_s_bc [B, C] F32 = sum over the N tokens
+ * of grad_out * branch (or NULL; needs gd_add_scaled_workspace_bytes(B, N, C)
+ * bytes of workspace; the caller folds it to s's broadcast shape).
+ * Deterministic.
+ */
+size_t gd_add_scaled_workspace_bytes(int64_t B, int64_t N, int C);
+gd_status gd_add_scaled_forward(gd_dtype x_dtype, const void* x, gd_dtype branch_dtype, const void* branch,
+                                const float* s, int64_t s_bstride, int s_cstride, int64_t B, int64_t N, int C,
+                                gd_dtype out_dtype, void* out, gd_stream_t stream);
+gd_status gd_add_scaled_backward(gd_dtype g_dtype, const void* grad_out, gd_dtype branch_dtype,
+                                 const void* branch, const float* s, int64_t s_bstride, int s_cstride,
+                                 int64_t B, int64_t N, int C, void* grad_branch, float* grad_s_bc,
+                                 void* workspace, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Hungarian matching (matcher.py:104-110)                                   */

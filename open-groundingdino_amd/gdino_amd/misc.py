@@ -3,11 +3,14 @@ groundingdino/util/misc.py and timm): NestedTensor, padding of image lists,
 inverse_sigmoid, distributed helpers, DropPath, trunc_normal_."""
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
 import torch.distributed as dist
 from torch import Tensor, nn
+
+from . import _lib
 
 
 _CONSTS = {}
@@ -175,15 +178,42 @@ def add_drop_path(x: Tensor, branch: Tensor, drop_prob: float = 0.0, training: b
     return _AddScaled.apply(x, branch, s)
 
 
+_p, _i, _i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+_lib.register("gd_add_scaled_forward", [_i, _p, _i, _p, _p, _i64, _i, _i64, _i64, _i, _i, _p, _p])
+_lib.register("gd_add_scaled_backward", [_i, _p, _i, _p, _p, _i64, _i, _i64, _i64, _i, _p, _p, _p, _p])
+
+
+def _scale_layout(x, s):
+    """(s as fp32 [Bs, 1, Cs], batch stride, channel stride) when the HIP
+    kernel (csrc/residual.hip) takes x [B, N, C] and this broadcast of s,
+    else None (the composition runs)."""
+    if not (_lib.enabled("addscaled") and _lib.on_device(x) and x.dim() == 3 and s.dim() <= 3):
+        return None
+    b, _, c = x.shape
+    s3 = s.reshape((1,) * (3 - s.dim()) + tuple(s.shape))
+    if c % 4 or c > 1024 or s3.shape[1] != 1 or s3.shape[0] not in (1, b) or s3.shape[2] not in (1, c):
+        return None
+    s32 = s3.detach().float().contiguous()
+    return s32, (s3.shape[2] if s3.shape[0] == b and b > 1 else 0), (1 if s3.shape[2] == c and c > 1 else 0)
+
+
+def _aligned(*ts):
+    return all(t.dtype in (torch.float32, torch.bfloat16) and t.data_ptr() % 16 == 0 and t.is_contiguous()
+               for t in ts)
+
+
 class _AddScaled(torch.autograd.Function):
     """x + branch * s, s broadcast per sample over the tokens ([B, 1, C] or
-    [B, 1, 1]; fp32 or branch's dtype).  Forward: one addcmul (outside
-    autocast, whose promotion would add a cast kernel for a bf16 branch).
-    Backward: d branch = g * s written straight in branch's dtype (one
-    kernel: mul into a bf16 out tensor), d s = sum over the tokens of
-    g * branch as a ones-vector GEMM over the [B, tokens, C] product instead
-    of a middle-dimension reduction (PyTorch's sum over dim 1 of a
-    [2, 22223, 256] tensor ran at ~0.35 TB/s: 130 us per fusion layer)."""
+    [B, 1, 1], or one scale for all samples; fp32 or branch's dtype).
+
+    On the GPU: one streaming kernel forward and one backward + a fixed-order
+    partial merge (csrc/residual.hip: d branch = g * s in branch's dtype and
+    d s = sum over the tokens of g * branch in the same pass over g).  The
+    composition (CPU, GDINO_DISABLE=addscaled): an addcmul forward (outside
+    autocast, whose promotion would add a cast kernel for a bf16 branch); a
+    mul into a branch-dtype tensor and a ones-vector GEMM over the g * branch
+    product backward (PyTorch's sum over dim 1 of a [2, 22223, 256] tensor ran
+    at ~0.35 TB/s)."""
 
     @staticmethod
     def forward(ctx, x, branch, s):
@@ -192,12 +222,29 @@ class _AddScaled(torch.autograd.Function):
         # would hold one activation per residual for nothing
         ctx.save_for_backward(branch if ctx.needs_input_grad[2] else None, s)
         ctx.branch_meta = (branch.shape, branch.dtype)
+        lay = _scale_layout(x, s) if x.shape == branch.shape else None
+        out_dtype = torch.promote_types(torch.promote_types(x.dtype, branch.dtype), s.dtype)
+        if lay is not None:
+            xc, bc = x.contiguous(), branch.contiguous()
+            out = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+            if _aligned(xc, bc, out):
+                s32, sbs, scs = lay
+                bsz, n, c = x.shape
+                _lib.call("gd_add_scaled_forward", _lib.dtype_code(xc), xc.data_ptr(), _lib.dtype_code(bc),
+                          bc.data_ptr(), s32.data_ptr(), sbs, scs, bsz, n, c, _lib.dtype_code(out),
+                          out.data_ptr(), _lib.stream_of(x),
+                          nbytes=x.numel() * (xc.element_size() + bc.element_size() + out.element_size()))
+                ctx.kernel = True
+                return out
+        ctx.kernel = False
         with torch.autocast(device_type=x.device.type, enabled=False):
             return torch.addcmul(x, branch, s)
 
     @staticmethod
     def backward(ctx, g):
         branch, s = ctx.saved_tensors
+        if ctx.kernel:
+            return _AddScaled._backward_kernel(ctx, g, branch, s)
         gb = gs = None
         if ctx.needs_input_grad[1]:
             shape, dtype = ctx.branch_meta
@@ -217,6 +264,44 @@ class _AddScaled(torch.autograd.Function):
                 gs = torch.bmm(p3.new_ones(b, 1, p3.shape[1]), p3)  # [b, 1, c]
                 gs = gs if cs == c else gs.sum(-1, keepdim=True)
             gs = gs.reshape(s.shape).to(s.dtype)
+        return g if ctx.needs_input_grad[0] else None, gb, gs
+
+    @staticmethod
+    def _backward_kernel(ctx, g, branch, s):
+        shape, dtype = ctx.branch_meta
+        bsz, n, c = shape
+        s32, sbs, scs = _scale_layout(g, s)
+        g = g.contiguous()
+        if g.dtype not in (torch.float32, torch.bfloat16):
+            g = g.float()
+        want_b, want_s = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        gb = torch.empty(shape, dtype=dtype, device=g.device) if want_b else None
+        gs_bc = ws = None
+        if want_s:
+            gs_bc = torch.empty(bsz, c, dtype=torch.float32, device=g.device)
+            fn = _lib.lib().gd_add_scaled_workspace_bytes
+            fn.restype, fn.argtypes = ctypes.c_size_t, [_i64, _i64, _i]
+            ws = torch.empty((int(fn(bsz, n, c)) + 3) // 4, dtype=torch.float32, device=g.device)
+            branch = branch.contiguous()
+        if (want_b or want_s) and _aligned(*[t for t in (g, gb, branch if want_s else None) if t is not None]):
+            _lib.call("gd_add_scaled_backward", _lib.dtype_code(g), g.data_ptr(), _lib.dtype_code(branch)
+                      if want_s else _lib.dtype_code(gb), _lib.ptr(branch if want_s else None), s32.data_ptr(),
+                      sbs, scs, bsz, n, c, _lib.ptr(gb), _lib.ptr(gs_bc), _lib.ptr(ws), _lib.stream_of(g),
+                      nbytes=g.numel() * (g.element_size() + (2 * gb.element_size() if want_b else 0)
+                                          + (branch.element_size() if want_s else 0)))
+        elif want_b or want_s:  # unaligned views: the composition
+            if want_b:
+                torch.mul(g, s, out=gb)
+            if want_s:
+                gs_bc = torch.mul(g, branch).float().sum(1)
+        gs = None
+        if want_s:
+            s3 = s.reshape((1,) * (3 - s.dim()) + tuple(s.shape))
+            if s3.shape[2] == 1:
+                gs_bc = gs_bc.sum(-1, keepdim=True)
+            if s3.shape[0] == 1:
+                gs_bc = gs_bc.sum(0, keepdim=True)
+            gs = gs_bc.reshape(s.shape).to(s.dtype)
         return g if ctx.needs_input_grad[0] else None, gb, gs
 
 

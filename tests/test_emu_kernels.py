@@ -826,3 +826,47 @@ def test_emulated_add_layernorm(rows, C, xd, rd):
         assert dr is None
     assert E.rel_err(dw, wd.grad) < 1e-5
     assert E.rel_err(db, bd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("n,c,bd,sshape,sd,xd", [
+    (37, 96, torch.bfloat16, (2, 1, 96), torch.float32, torch.float32),    # layer scale x drop path
+    (300, 256, torch.bfloat16, (2, 1, 1), torch.bfloat16, torch.float32),  # drop path only, bf16 mask
+    (29, 64, torch.float32, (64,), torch.float32, torch.float32),          # one gamma for all samples
+    (50, 128, torch.bfloat16, (1, 1, 128), torch.float32, torch.bfloat16),
+    (11, 192, torch.bfloat16, (2, 1, 1), torch.bfloat16, torch.bfloat16),  # bf16 out
+])
+def test_emulated_add_scaled(n, c, bd, sshape, sd, xd, monkeypatch):
+    """csrc/residual.hip (x + branch * s and its backward) through the
+    product's autograd function vs the addcmul composition it replaces
+    (GDINO_DISABLE=addscaled): forward and d branch within one rounding of
+    the output dtype, d x = g, d s (the token reduction) within fp32
+    summation-order noise."""
+    from emu_product import emulated_product
+    from gdino_amd.misc import _AddScaled
+    g = torch.Generator().manual_seed(n * c)
+    x = torch.randn(2, n, c, generator=g).to(xd)
+    br = torch.randn(2, n, c, generator=g).to(bd)
+    s = (torch.rand(sshape, generator=g) + 0.5).to(sd)
+    go_seed = torch.randn(2, n, c, generator=g)
+
+    def run(disable):
+        if disable:
+            monkeypatch.setenv("GDINO_DISABLE", "addscaled")
+        else:
+            monkeypatch.delenv("GDINO_DISABLE", raising=False)
+        xx, bb, ss = (t.clone().requires_grad_(True) for t in (x, br, s))
+        with emulated_product():
+            out = _AddScaled.apply(xx, bb, ss)
+            out.backward(go_seed.to(out.dtype))
+        return out.detach(), xx.grad, bb.grad, ss.grad
+
+    got, ref = run(False), run(True)
+    assert got[0].dtype == ref[0].dtype
+    for name, a, b in zip(("out", "dx", "dbranch", "ds"), got, ref):
+        assert a.dtype == b.dtype and a.shape == b.shape, name
+        a, b = a.double(), b.double()
+        tol = 1e-5 if a.dtype == torch.float32 else (2 ** -7 if name in ("out", "dbranch") else 1e-2)
+        if name == "ds":
+            tol = 1e-4 if s.dtype == torch.float32 else 1e-2
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        assert err <= tol, (name, err)

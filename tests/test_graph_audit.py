@@ -24,3 +24,21 @@ def test_forward_core_builds_no_tensor_from_host_data(monkeypatch):
     audit.main()
     bad = {k: n for k, n in hits["audit"].hits.items() if k[0] != "_local_scalar_dense"}
     assert not bad, bad
+
+
+def test_whole_step_body_builds_no_tensor_from_host_data(monkeypatch):
+    """The region gdino_amd.stepgraph captures (forward, loss_prepared with
+    device matching, weighted loss, backward, clipping): no host-data tensor
+    and no device move (the oracle MSDA's own scalar reads aside)."""
+    import graph_h2d_audit as audit
+    hits = {}
+    monkeypatch.setattr(sys, "argv", ["graph_h2d_audit.py", "--whole-step"])
+    orig = audit.Audit.__init__
+
+    def init(self):
+        orig(self)
+        hits["audit"] = self
+    monkeypatch.setattr(audit.Audit, "__init__", init)
+    audit.main()
+    bad = {k: n for k, n in hits["audit"].hits.items() if k[0] != "_local_scalar_dense"}
+    assert not bad, bad

@@ -12,7 +12,13 @@ CPU tests do: device changes cannot show there, host-data creation and
 scalar reads can.  With --device cuda the HIP path itself runs under bf16
 autocast, as bench.py's train step does.
 
-    python tools/graph_h2d_audit.py [--device cuda] [--height H --width W]
+    python tools/graph_h2d_audit.py [--device cuda] [--height H --width W] [--whole-step]
+
+--whole-step audits the region gdino_amd.stepgraph captures instead: the
+forward, SetCriterion.loss_prepared (device matching; on the CPU the solver
+is scipy's, outside the audit), the weighted loss, the backward and the
+gradient clipping (the captured fused AdamW is PyTorch's own capturable
+kernel and is not run here).
 """
 import argparse
 import os
@@ -39,9 +45,12 @@ class Audit(TorchDispatchMode):
     def __init__(self):
         super().__init__()
         self.hits = {}
+        self.paused = False
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
+        if self.paused:
+            return func(*args, **kwargs)
         name = func._schema.name.split("::")[-1]
         hit = name in FLAG
         if name in ("_to_copy", "copy_"):
@@ -59,7 +68,10 @@ def main():
     ap.add_argument("--height", type=int, default=256)
     ap.add_argument("--width", type=int, default=320)
     ap.add_argument("--device", default="cpu")
+    ap.add_argument("--whole-step", action="store_true")
     a = ap.parse_args()
+    if a.whole_step:
+        return whole_step(a)
     dev = torch.device(a.device)
     if dev.type == "cpu":
         from oracle_hooks import oracle_msda
@@ -89,6 +101,72 @@ def main():
             loss.backward()
     if not audit.hits:
         print("graph_h2d_audit: forward_core + backward: no host-data tensors, scalar reads or device moves")
+        return 0
+    for (name, site), n in sorted(audit.hits.items(), key=lambda kv: kv[0][1]):
+        print(f"{n:4d} x {name:22s} {site}")
+    return 1
+
+
+def whole_step(a):
+    """The step graph's body (stepgraph.TrainStepGraph._body without the
+    optimizer step) under the audit, on the CPU with the HIP-only ops routed
+    to their oracles and the device LSA replaced by scipy (not audited)."""
+    import numpy as np
+    from scipy.optimize import linear_sum_assignment
+    from oracle_hooks import oracle_msda
+    from gdino_amd import lsap
+    from gdino_amd.config import make_args
+    from gdino_amd.stepgraph import TrainStepGraph
+    from gdino_amd.train import build_training, synthetic_batch
+
+    dev = torch.device(a.device)
+    torch.manual_seed(0)
+    model, criterion, _, _ = build_training(make_args(device=str(dev)), dev)
+    model.train()
+    audit = Audit()
+
+    def host_lsa(cost, sizes, status=None):
+        audit.paused = True
+        try:
+            p, q, k = cost.shape
+            rows = torch.full((p, k), -1, dtype=torch.int64)
+            cols = torch.full((p, k), -1, dtype=torch.int64)
+            c = cost.detach().double().numpy()
+            for i, n in enumerate(sizes.tolist()):
+                r, cc = linear_sum_assignment(np.asarray(c[i, :, :n]))
+                rows[i, :len(r)], cols[i, :len(r)] = torch.from_numpy(r), torch.from_numpy(cc)
+            return rows.to(cost.device), cols.to(cost.device)
+        finally:
+            audit.paused = False
+
+    class NoStep:
+        def step(self):
+            pass
+
+        def zero_grad(self, set_to_none=True):
+            model.zero_grad(set_to_none=set_to_none)
+
+    g = TrainStepGraph.__new__(TrainStepGraph)
+    g.model, g.criterion, g.optimizer = model, criterion, NoStep()
+    on_gpu = dev.type == "cuda"
+    # on the GPU the product path itself (bf16 autocast, the device LSA)
+    g.clip_max_norm, g.amp_dtype, g.grad_sync, g.kmax_multiple = 0.1, (torch.bfloat16 if on_gpu else None), None, 8
+    samples, targets, captions, cats = synthetic_batch(2, a.height, a.width, n_boxes=4, n_tokens=64, seed=0,
+                                                       device=dev)
+    saved = lsap.linear_sum_assignment_batched
+    if not on_gpu:
+        lsap.linear_sum_assignment_batched = host_lsa
+    import contextlib
+    try:
+        with (contextlib.nullcontext() if on_gpu else oracle_msda()):
+            inputs = g._prepare(samples, targets, captions, cats)
+            g._body(inputs)  # warm-up: device constants, caches
+            with audit:
+                g._body(inputs)
+    finally:
+        lsap.linear_sum_assignment_batched = saved
+    if not audit.hits:
+        print("graph_h2d_audit: whole step body: no host-data tensors, scalar reads or device moves")
         return 0
     for (name, site), n in sorted(audit.hits.items(), key=lambda kv: kv[0][1]):
         print(f"{n:4d} x {name:22s} {site}")
