@@ -275,31 +275,60 @@ wgrad_tr_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, const
   }
 }
 
-// out[b] = sum over splits of the partials (4 columns per thread), written in
-// fp32 or bf16 with batch stride ob; db (batch 1) likewise
+// out[b] = sum over splits of the partials, written in fp32 or bf16 with
+// batch stride ob; db (batch 1) likewise.  A workgroup owns 32 float4
+// column groups; its 8 thread groups each sum every 8th split (split k to
+// group k % 8) and the 8 group sums are added in LDS in group order: a fixed
+// order (deterministic) and 8x the threads of one thread per float4, whose
+// 65-workgroup grid for a 256 x 256 weight left most CUs idle on the serial
+// split loop (11 us for ~25 MB of L2 / MALL-resident partials).
+constexpr int kRedCols = 32, kRedGroups = 8;
+
 template <typename TO>
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ part_b, int splits, int batch,
                     int O, int I, TO* __restrict__ out, int64_t ob, float* __restrict__ db) {
-  const int64_t t = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  __shared__ float4 red[kRedGroups][kRedCols];
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+  const int64_t t = int64_t(blockIdx.x) * kRedCols + col;
   const int64_t nw4 = int64_t(O) * I / 4;  // float4 groups per batch item
+  const int64_t nb4 = db ? O / 4 : 0;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* src = nullptr;
+  int64_t stride = 0;
   if (t < nw4 * batch) {
     const int64_t b = t / nw4, e = t - b * nw4;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(part_w)[(b * splits + k) * nw4 + e];
+    src = reinterpret_cast<const float4*>(part_w) + b * splits * nw4 + e;
+    stride = nw4;
+  } else if (t < nw4 * batch + nb4) {
+    src = reinterpret_cast<const float4*>(part_b) + (t - nw4 * batch);
+    stride = nb4;
+  }
+  if (src) {
+    for (int k = grp; k < splits; k += kRedGroups) {
+      const float4 v = src[int64_t(k) * stride];
       s.x += v.x;
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
     }
-    TO* o = out + b * ob + e * 4;
-    st4(o, s);
-  } else if (db && t < nw4 * batch + O) {
-    const int o = int(t - nw4 * batch);
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part_b[int64_t(k) * O + o];
-    db[o] = s;
+  }
+  red[grp][col] = s;
+  __syncthreads();
+  if (grp != 0 || !src) return;
+#pragma unroll
+  for (int g = 1; g < kRedGroups; ++g) {
+    const float4 v = red[g][col];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  if (t < nw4 * batch) {
+    const int64_t b = t / nw4, e = t - b * nw4;
+    st4(out + b * ob + e * 4, s);
+  } else {
+    st4(db + (t - nw4 * batch) * 4, s);
   }
 }
 
@@ -369,8 +398,8 @@ extern "C" gd_status gd_wgrad_batched(gd_dtype dt, const void* grad_y, int64_t l
                        grad_b ? part_b : nullptr);
   }
   GD_LAUNCH_CHECK("wgrad");
-  const int64_t n = int64_t(O) * I / 4 * batch + (grad_b ? O : 0);
-  const dim3 rg(unsigned((n + 255) / 256));
+  const int64_t n = int64_t(O) * I / 4 * batch + (grad_b ? O / 4 : 0);  // float4 groups (O % 16 == 0)
+  const dim3 rg(unsigned((n + kRedCols - 1) / kRedCols));
   if (out_dtype == GD_F32)
     hipLaunchKernelGGL((wgrad_reduce_kernel<float>), rg, dim3(256), 0, s, part_w, part_b, splits, batch, O, I,
                        (float*)out, batch_stride_out, grad_b);
