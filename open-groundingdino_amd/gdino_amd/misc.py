@@ -3,6 +3,8 @@ groundingdino/util/misc.py and timm): NestedTensor, padding of image lists,
 inverse_sigmoid, distributed helpers, DropPath, trunc_normal_."""
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import ctypes
 from typing import Optional
 
@@ -45,18 +47,41 @@ def topk_indices(x: Tensor, k: int) -> Tensor:
     return torch.topk(x, k, dim=1)[1]
 
 
+_PADDING_FREE = contextvars.ContextVar("gd_padding_free", default=False)
+
+
+@contextlib.contextmanager
+def no_padding(flag: bool = True):
+    """Within: the batch's padding mask is known on the host to be all False
+    (every image fills the padded canvas), so masking by it is the identity
+    and the deformable attention skips its value masked_fill (forward and
+    backward: three passes over a [B, S, 256] tensor per MSDA layer)."""
+    tok = _PADDING_FREE.set(bool(flag))
+    try:
+        yield
+    finally:
+        _PADDING_FREE.reset(tok)
+
+
+def padding_free() -> bool:
+    return _PADDING_FREE.get()
+
+
 class NestedTensor:
     """Batched images + padding mask (True on padded pixels).
     Contract of groundingdino/util/misc.py:399-480; the model also accepts any
-    object with ``.tensors`` and ``.mask`` (e.g. the reference's own class)."""
+    object with ``.tensors`` and ``.mask`` (e.g. the reference's own class).
+    ``padding_free``: the host knows the mask is all False (no image was
+    padded), which lets the model skip masking by it."""
 
-    def __init__(self, tensors: Tensor, mask: Optional[Tensor]):
+    def __init__(self, tensors: Tensor, mask: Optional[Tensor], padding_free: bool = False):
         self.tensors = tensors
         self.mask = mask
+        self.padding_free = bool(padding_free)
 
     def to(self, device, non_blocking=False):
         m = None if self.mask is None else self.mask.to(device, non_blocking=non_blocking)
-        return NestedTensor(self.tensors.to(device, non_blocking=non_blocking), m)
+        return NestedTensor(self.tensors.to(device, non_blocking=non_blocking), m, self.padding_free)
 
     def decompose(self):
         return self.tensors, self.mask
@@ -64,7 +89,8 @@ class NestedTensor:
     def pin_memory(self):
         """DataLoader(pin_memory=True) hook: page-locked host tensors, so the
         host->device copy of the batch is asynchronous."""
-        return NestedTensor(self.tensors.pin_memory(), None if self.mask is None else self.mask.pin_memory())
+        return NestedTensor(self.tensors.pin_memory(), None if self.mask is None else self.mask.pin_memory(),
+                            self.padding_free)
 
     @property
     def device(self):
@@ -110,7 +136,7 @@ def nested_tensor_from_tensor_list(tensor_list) -> NestedTensor:
     (groundingdino/util/misc.py:483-506)."""
     if isinstance(tensor_list, Tensor) and tensor_list.dim() == 4:
         b, _, h, w = tensor_list.shape
-        return NestedTensor(tensor_list, torch.zeros((b, h, w), dtype=torch.bool, device=tensor_list.device))
+        return NestedTensor(tensor_list, torch.zeros((b, h, w), dtype=torch.bool, device=tensor_list.device), True)
     if tensor_list[0].ndim != 3:
         raise ValueError("not supported")
     c = max(t.shape[0] for t in tensor_list)
@@ -122,7 +148,7 @@ def nested_tensor_from_tensor_list(tensor_list) -> NestedTensor:
     for i, img in enumerate(tensor_list):
         batch[i, : img.shape[0], : img.shape[1], : img.shape[2]].copy_(img)
         mask[i, : img.shape[1], : img.shape[2]] = False
-    return NestedTensor(batch, mask)
+    return NestedTensor(batch, mask, all(tuple(t.shape[1:]) == (h, w) for t in tensor_list))
 
 
 def inverse_sigmoid(x: Tensor, eps: float = 1e-3) -> Tensor:

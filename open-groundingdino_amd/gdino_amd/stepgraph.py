@@ -34,6 +34,7 @@ import sys
 import time
 
 from . import castcache
+from .misc import no_padding
 from .train import BucketedGradSync, weighted_loss
 
 _VERBOSE = os.environ.get("GDINO_STEPGRAPH_VERBOSE") == "1"
@@ -125,12 +126,14 @@ class TrainStepGraph:
         return tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(inputs.items()))
 
     # -------------------------------------------------------------- step
-    def _body(self, inp):
+    def _body(self, inp, padding_free=False):
         """forward + loss + backward + all-reduce + clip + optimizer step;
-        only device work, no host synchronisation."""
+        only device work, no host synchronisation.  ``padding_free``: the
+        batch's image mask is all False (part of the graph's signature)."""
         model, crit = self.model, self.criterion
         dev_type = inp["images"].device.type
-        with torch.autocast(device_type=dev_type, dtype=self.amp_dtype, enabled=self.amp_dtype is not None):
+        with torch.autocast(device_type=dev_type, dtype=self.amp_dtype, enabled=self.amp_dtype is not None), \
+                no_padding(padding_free):
             core = model.forward_core(inp["images"], inp["mask"], inp["input_ids"], inp["token_type_ids"],
                                       inp["text_token_mask"], inp["self_masks"], inp["position_ids"])
             outputs = model.assemble_outputs(core)
@@ -147,7 +150,7 @@ class TrainStepGraph:
         self.optimizer.step()
         return loss.detach(), {k: v.detach() for k, v in loss_dict.items()}
 
-    def _capture(self, key, inputs):
+    def _capture(self, key, inputs, padding_free=False):
         c = _Captured()
         for k, v in inputs.items():
             c.inputs[k] = _static_like(v)
@@ -165,7 +168,7 @@ class TrainStepGraph:
             for i in range(self.warmup):
                 if self.grad_sync is None:
                     self.optimizer.zero_grad(set_to_none=True)
-                self._body(c.inputs)
+                self._body(c.inputs, padding_free)
                 if _VERBOSE:
                     side.synchronize()
                     _log(f"warm-up step {i} done")
@@ -188,7 +191,7 @@ class TrainStepGraph:
         # capture reuse memory an earlier graph's replays still write)
         _log("capture begins")
         with torch.cuda.graph(c.graph, stream=side):
-            c.loss, c.loss_dict = self._body(c.inputs)
+            c.loss, c.loss_dict = self._body(c.inputs, padding_free)
         torch.cuda.current_stream().wait_stream(side)
         _log(f"captured ({c.graph.__class__.__name__})")
         self.graphs[key] = c
@@ -201,10 +204,11 @@ class TrainStepGraph:
         while len(self._inflight) >= self.max_inflight:
             self._inflight.pop(0).synchronize()
         inputs = self._prepare(samples, targets, captions, cat_lists)
-        key = self._signature(inputs)
+        pf = bool(getattr(samples, "padding_free", False))
+        key = self._signature(inputs) + (("padding_free", pf),)
         c = self.graphs.get(key)
         if c is None:
-            c = self._capture(key, inputs)
+            c = self._capture(key, inputs, pf)
         else:
             c.load(inputs)
         c.graph.replay()

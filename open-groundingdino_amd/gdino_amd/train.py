@@ -93,7 +93,7 @@ def synthetic_batch(bs: int, height: int, width: int, n_boxes: int = 8, n_tokens
                         "orig_size": torch.tensor([height, width], device=device)})
         captions.append(caption)
         cat_lists.append(cats)
-    return NestedTensor(imgs, mask), targets, captions, cat_lists
+    return NestedTensor(imgs, mask, padding_free=True), targets, captions, cat_lists
 
 
 # --------------------------------------------------------------- optimizer

@@ -36,7 +36,7 @@ from torch import nn
 
 from gdino_amd import box_ops, castcache
 from gdino_amd.conv import GemmConv2d
-from gdino_amd.misc import (NestedTensor, get_world_size, inverse_sigmoid, is_dist_avail_and_initialized,
+from gdino_amd.misc import (NestedTensor, no_padding, get_world_size, inverse_sigmoid, is_dist_avail_and_initialized,
                             nested_tensor_from_tensor_list)
 from gdino_amd.tokenizer import get_pretrained_language_model, get_tokenlizer
 
@@ -258,8 +258,10 @@ class GroundingDINO(nn.Module):
         device = samples.tensors.device
         text, one_hot_token = self.prepare_text(captions, device, kw.get("prepared_text"))
         core = self._graphed_core if getattr(self, "_graphed_core", None) is not None else self.forward_core
-        outs = core(samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
-                    text["text_token_mask"], text["self_masks"], text["position_ids"])
+        # (a graphed core keeps the masking it was captured with)
+        with no_padding(getattr(samples, "padding_free", False)):
+            outs = core(samples.tensors, samples.mask, text["input_ids"], text["token_type_ids"],
+                        text["text_token_mask"], text["self_masks"], text["position_ids"])
         return self.assemble_outputs(outs, one_hot_token)
 
     def assemble_outputs(self, core_outputs, one_hot_token=None):

@@ -32,6 +32,7 @@ import torch.nn as nn
 from torch.nn.init import constant_, xavier_uniform_
 
 from gdino_amd import castcache, msda_prologue
+from gdino_amd.misc import padding_free
 
 from .ops.functions.ms_deform_attn_func import MSDeformAttnFunction
 
@@ -91,7 +92,7 @@ def msda_attend(mod, query, value, reference_points, spatial_shapes, level_start
     bs, num_query, _ = query.shape
     _, num_value, _ = value.shape
     value = mod.value_proj(value)
-    if key_padding_mask is not None:
+    if key_padding_mask is not None and not padding_free():  # (an all-False mask: identity)
         value = value.masked_fill(key_padding_mask[..., None], 0.0)
     value = value.view(bs, num_value, num_heads, -1)
     offsets, attn = castcache.linear_shared_input(query, (mod.sampling_offsets, mod.attention_weights))

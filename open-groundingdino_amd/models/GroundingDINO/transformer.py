@@ -14,6 +14,7 @@ Host-side changes, all behaviour-preserving:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import List, Optional
 
@@ -24,7 +25,7 @@ from torch import Tensor, nn
 from gdino_amd import kernels
 from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
-from gdino_amd.misc import device_const, inverse_sigmoid, topk_indices
+from gdino_amd.misc import device_const, inverse_sigmoid, no_padding, padding_free, topk_indices
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
@@ -38,7 +39,11 @@ MSDA_IDENTITY_ADD = os.environ.get("GDINO_MSDA_SEMANTICS", "mmcv") == "mmcv"
 
 
 def _ckpt(fn, *args):
-    return checkpoint.checkpoint(fn, *args, use_reentrant=False)
+    # the recompute (in backward, outside the forward's no_padding context)
+    # must take the forward's masking decision: same ops, same saved tensors
+    pf = padding_free()
+    return checkpoint.checkpoint(fn, *args, use_reentrant=False,
+                                 context_fn=lambda: (contextlib.nullcontext(), no_padding(pf)))
 
 
 class Transformer(nn.Module):

@@ -382,6 +382,41 @@ def test_activation_checkpointing_does_not_change_the_step():
     set_activation_checkpointing(model, True)
 
 
+def test_padding_free_batch_skips_only_an_identity_mask():
+    """A batch whose images all fill the canvas (NestedTensor.padding_free:
+    known on the host) skips the deformable attention's value masked_fill;
+    the mask is all False there, so the loss is bitwise that of the masked run
+    and every gradient agrees to fp32 summation order.  nested_tensor_from_tensor_list sets the flag
+    only when no image was padded."""
+    from gdino_amd.config import make_args
+    from gdino_amd.misc import NestedTensor, nested_tensor_from_tensor_list
+    from gdino_amd.train import build_training, synthetic_batch, weighted_loss
+    torch.manual_seed(0)
+    model, criterion, _, _ = build_training(make_args(device="cpu", num_queries=60, enc_layers=1, dec_layers=1),
+                                            "cpu")
+    model.train()
+    samples, targets, caps, cats = synthetic_batch(2, 96, 128, n_boxes=3, n_tokens=30, seed=3, device="cpu")
+    assert samples.padding_free and not bool(samples.mask.any())
+    res = {}
+    for pf in (True, False):
+        model.zero_grad(set_to_none=True)
+        torch.manual_seed(123)
+        with oracle_msda():
+            out = model(NestedTensor(samples.tensors, samples.mask, pf), captions=caps)
+            loss = weighted_loss(criterion(out, targets, cats, caps), criterion.weight_dict)
+            loss.backward()
+        res[pf] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert torch.equal(res[True][0], res[False][0])
+    for n, g in res[True][1].items():
+        # (the autograd engine may sum a tensor's incoming gradients in
+        # another order without the masked_fill node: fp32 rounding apart)
+        r = res[False][1][n]
+        assert float((g - r).abs().max()) <= 1e-6 * float(r.abs().max().clamp_min(1e-30)), n
+    a, b = torch.zeros(3, 8, 8), torch.zeros(3, 6, 8)
+    assert nested_tensor_from_tensor_list([a, a]).padding_free
+    assert not nested_tensor_from_tensor_list([a, b]).padding_free
+
+
 def test_group_shadows_make_the_fused_projection_cat_a_view(built):
     """castcache group shadows: the shadows of the parameters a fused
     projection concatenates (MSDA offsets | weights, BiAttention v | values_v,
