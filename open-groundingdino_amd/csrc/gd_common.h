@@ -79,6 +79,34 @@ __device__ __forceinline__ float dpp(float v) {
   return __builtin_amdgcn_update_dpp(0.f, v, CTRL, 0xf, 0xf, false);
 }
 
+// ---- fills as kernels ------------------------------------------------------
+// Every buffer the kernels need pre-filled is filled by this kernel, not by
+// hipMemsetAsync: inside a captured HIP graph a memset becomes a memset node,
+// and the step graph's replays faulted (illegal address / hangs) while its
+// eager warm-ups of the same work ran clean -- a kernel node is ordered like
+// every other kernel of the stream.  bytes: a multiple of 4.
+namespace {
+__global__ void __launch_bounds__(256) fill_u32_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t v, int vec) {
+  const int64_t n4 = vec ? n / 4 : 0;
+  const uint4 v4 = make_uint4(v, v, v, v);
+  const int64_t stride = int64_t(gridDim.x) * 256;
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<uint4*>(p)[i] = v4;
+  for (int64_t i = n4 * 4 + int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+}  // namespace
+
+// fill bytes / 4 words at p with v (16-byte aligned p: vector stores)
+inline hipError_t fill_u32_async(void* p, uint32_t v, size_t bytes, hipStream_t s) {
+  const int64_t n = int64_t(bytes / 4);
+  if (n == 0) return hipSuccess;
+  const int vec = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  int64_t blocks = ((vec ? n / 4 : n) + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  hipLaunchKernelGGL(fill_u32_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, static_cast<uint32_t*>(p), n, v, vec);
+  return hipGetLastError();
+}
+
 }  // namespace gd
 
 // integer tuning / A-B switch from the environment (host side)

@@ -261,8 +261,8 @@ extern "C" gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, 
              "add_layernorm_backward: grad_weight and grad_bias are requested together");
   if (rows == 0) {
     hipStream_t s = as_hip(stream);
-    if (grad_weight) GD_HIP_CHECK(hipMemsetAsync(grad_weight, 0, sizeof(float) * C, s));
-    if (grad_bias) GD_HIP_CHECK(hipMemsetAsync(grad_bias, 0, sizeof(float) * C, s));
+    if (grad_weight) GD_HIP_CHECK(fill_u32_async(grad_weight, 0u, sizeof(float) * C, s));
+    if (grad_bias) GD_HIP_CHECK(fill_u32_async(grad_bias, 0u, sizeof(float) * C, s));
     return GD_OK;
   }
   GD_REQUIRE(x && grad_y && mean && rstd && grad_x, "add_layernorm_backward: null pointer");

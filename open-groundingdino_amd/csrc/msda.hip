@@ -191,7 +191,7 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
   const size_t nval = size_t(N) * S * M * D;
   if (nval) {
     GD_REQUIRE(grad_value && value, "msda_backward: null value / grad_value");
-    GD_HIP_CHECK(hipMemsetAsync(grad_value, 0, nval * acc, s));
+    GD_HIP_CHECK(fill_u32_async(grad_value, 0u, nval * acc, s));
   }
   if (units == 0) return GD_OK;
   GD_REQUIRE(grad_out && loc && attn && grad_loc && grad_attn && shapes && lsi,
@@ -318,8 +318,8 @@ extern "C" gd_status gd_msda_backward_geom(gd_dtype dt, const void* value,
     return GD_OK;
   }
   const size_t nloc = size_t(units) * L * P;
-  GD_HIP_CHECK(hipMemsetAsync(grad_loc, 0, nloc * 2 * acc, s));
-  GD_HIP_CHECK(hipMemsetAsync(grad_attn, 0, nloc * acc, s));
+  GD_HIP_CHECK(fill_u32_async(grad_loc, 0u, nloc * 2 * acc, s));
+  GD_HIP_CHECK(fill_u32_async(grad_attn, 0u, nloc * acc, s));
   if (dt == GD_F32) {
     hipLaunchKernelGGL((msda_bwd_generic<float, float>), dim3(grid_for(total, 256)), dim3(256), 0, s,
                      (const float*)value, shapes, lsi, (const float*)loc, (const float*)attn,
@@ -518,7 +518,7 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
   int4* scr = reinterpret_cast<int4*>(w + pl.o_scr);
   float* part = reinterpret_cast<float*>(w + pl.o_part);
   const int units = pl.nsamples / 16;
-  GD_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * size_t(pl.ncells + 2), s));
+  GD_HIP_CHECK(fill_u32_async(cnt, 0u, sizeof(int) * size_t(pl.ncells + 2), s));
   int* stat = cnt + pl.ncells;  // coarse runs / coarse samples of the first count blocks
   if (units > 0) {
     // coarse-level counts through a per-workgroup LDS histogram when both
@@ -569,7 +569,7 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       // forces K1's regardless of run length -- A/B)
       const int kenv = env_int("GD_MSDA_COUNT_PRIV", 1);
       const int kpriv = (Lq >= 64 && (hp && !pipe ? 4 : 2) * kc23 <= kCountBins && kenv != 0) ? 1 : 0;
-      if (kpriv && kenv == 2) GD_HIP_CHECK(hipMemsetAsync(stat, 0x10, sizeof(int), s));  // runs >> samples
+      if (kpriv && kenv == 2) GD_HIP_CHECK(fill_u32_async(stat, 0x10101010u, sizeof(int), s));  // runs >> samples
       // locations loaded level by level (default; 146 instead of 192 VGPRs:
       // 3 waves per SIMD): 345 -> 315 us at the init geometry, 510 -> 475 us
       // on a 2-px spread (profiles/r03g); GD_MSDA_SORTED_LL=0: all 48

@@ -212,7 +212,7 @@ extern "C" gd_status gd_add_scaled_backward(gd_dtype g_dtype, const void* grad_o
              "add_scaled_backward: dtypes %d/%d (F32, BF16)", int(g_dtype), int(branch_dtype));
   hipStream_t st = as_hip(stream);
   if (B * N == 0) {
-    if (grad_s_bc) GD_HIP_CHECK(hipMemsetAsync(grad_s_bc, 0, sizeof(float) * size_t(B) * C, st));
+    if (grad_s_bc) GD_HIP_CHECK(fill_u32_async(grad_s_bc, 0u, sizeof(float) * size_t(B) * C, st));
     return GD_OK;
   }
   GD_REQUIRE(grad_out && s && (grad_branch || grad_s_bc), "add_scaled_backward: null pointer");

@@ -1,0 +1,86 @@
+"""Are memset / memcpy nodes of a captured HIP graph ordered against the
+kernel nodes around them on replay?  (The whole-step graph faulted on replay
+while eager runs of the same work were clean; the HIP library's buffers that
+need zeros were hipMemsetAsync'd inside the capture.)
+
+Per replay, on one capturing stream:
+  memset probe:  fill kernel Z := 7  ->  hipMemsetAsync(Z, 0)  ->  kernel Z += 1
+                 ->  bad += count(Z != 1)
+  memcpy probe:  kernel A := step    ->  hipMemcpyAsync(B <- A) ->  kernel
+                 bad += count(B != step); step += 1
+A long GEMM precedes each probe so that the node before the memset / memcpy
+is still running when the next node could start.  No index is derived from
+the probed data: a reordering shows as a nonzero count, never as a fault.
+
+    python tools/graph_node_order_probe.py [--replays 300] [--mb 64]
+"""
+import argparse
+import ctypes
+import json
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--replays", type=int, default=300)
+    ap.add_argument("--mb", type=float, default=64.0)
+    a = ap.parse_args()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemsetAsync.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    dev = torch.device("cuda")
+    n = int(a.mb * 2 ** 20 / 4)
+    z = torch.empty(n, dtype=torch.float32, device=dev)
+    A = torch.empty(n, dtype=torch.float32, device=dev)
+    B = torch.empty(n, dtype=torch.float32, device=dev)
+    x = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
+    step = torch.zeros((), dtype=torch.float32, device=dev)
+    bad_set = torch.zeros((), dtype=torch.int64, device=dev)
+    bad_cpy = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def body():
+        s = torch.cuda.current_stream().cuda_stream
+        torch.mm(x, x, out=y)                      # a long kernel first
+        z.fill_(7.0)
+        assert hip.hipMemsetAsync(z.data_ptr(), 0, z.numel() * 4, s) == 0
+        z.add_(1.0)
+        bad_set.add_((z != 1.0).sum())
+        torch.mm(x, x, out=y)
+        A.copy_(step.expand_as(A))                 # a kernel (expand: not a memcpy)
+        assert hip.hipMemcpyAsync(B.data_ptr(), A.data_ptr(), A.numel() * 4, 3, s) == 0  # D2D
+        bad_cpy.add_((B != step).sum())
+        step.add_(1.0)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        body()  # eager once
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    eager = (int(bad_set), int(bad_cpy))
+    bad_set.zero_()
+    bad_cpy.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        body()
+    torch.cuda.synchronize()
+    for i in range(a.replays):
+        g.replay()
+        if i % 50 == 49:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    back = (int(bad_set), int(bad_cpy))
+    bad_set.zero_()
+    bad_cpy.zero_()
+    for i in range(a.replays):
+        g.replay()
+        torch.cuda.synchronize()
+    synced = (int(bad_set), int(bad_cpy))
+    print(json.dumps({"eager_bad": eager, "replays": a.replays, "back_to_back_bad(memset, memcpy)": back,
+                      "synced_bad(memset, memcpy)": synced}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
