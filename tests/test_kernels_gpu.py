@@ -674,3 +674,40 @@ def test_tn_matmul_biattention_shape():
     torch.cuda.synchronize()
     assert out.dtype == torch.bfloat16
     assert _rel(out.cpu(), a.double().transpose(-1, -2) @ b.double()) < 1e-2
+
+
+@pytest.mark.parametrize("shape,bd,sshape,sd", [
+    ((2, 22223, 256), torch.bfloat16, (2, 1, 256), torch.float32),   # BiAttention fusion: gamma x drop path
+    ((2, 256, 256), torch.bfloat16, (2, 1, 256), torch.float32),     # its text side
+    ((2, 66800, 96), torch.bfloat16, (2, 1, 1), torch.bfloat16),     # Swin-T stage 0 drop path
+    ((2, 4200, 384), torch.bfloat16, (2, 1, 1), torch.bfloat16),
+])
+def test_add_scaled_matches_composition(shape, bd, sshape, sd, monkeypatch):
+    """csrc/residual.hip through misc._AddScaled against the addcmul
+    composition (GDINO_DISABLE=addscaled) on the same inputs: output and
+    d branch within one rounding of their dtype, d s within fp32
+    summation-order noise, d x = g exactly."""
+    from gdino_amd.misc import _AddScaled
+    g = torch.Generator().manual_seed(shape[1])
+    x = torch.randn(shape, generator=g).to(DEV)
+    br = torch.randn(shape, generator=g).to(DEV, bd)
+    s = (torch.rand(sshape, generator=g) + 0.5).to(DEV, sd)
+    go = torch.randn(shape, generator=g).to(DEV)
+
+    def run(disable):
+        if disable:
+            monkeypatch.setenv("GDINO_DISABLE", "addscaled")
+        else:
+            monkeypatch.delenv("GDINO_DISABLE", raising=False)
+        xx, bb, ss = (t.clone().requires_grad_(True) for t in (x, br, s))
+        out = _AddScaled.apply(xx, bb, ss)
+        out.backward(go.to(out.dtype))
+        torch.cuda.synchronize()
+        return out.detach(), xx.grad, bb.grad, ss.grad
+
+    got, ref = run(False), run(True)
+    for name, a, b in zip(("out", "dx", "dbranch", "ds"), got, ref):
+        assert a.dtype == b.dtype and a.shape == b.shape, name
+        tol = {"out": 1e-6 if a.dtype == torch.float32 else 2 ** -7, "dx": 0.0,
+               "dbranch": 2 ** -7, "ds": 1e-4 if sd == torch.float32 else 1e-2}[name]
+        assert _rel(a, b) <= tol, (name, _rel(a, b))
