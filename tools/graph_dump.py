@@ -7,8 +7,9 @@ sizes -- the nodes a replay executes that the eager warm-ups did not show.
 """
 import argparse
 import collections
+import ctypes
+import json
 import os
-import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--full", action="store_true", help="the bench's shapes (default: the step-graph test's)")
     ap.add_argument("--ckpt", type=int, default=1)
-    ap.add_argument("--out", default="gpurun_out/graph.dot")
+    ap.add_argument("--out", default="gpurun_out/graph_nodes.txt")
     a = ap.parse_args()
     from gdino_amd.config import make_args
     from gdino_amd.stepgraph import TrainStepGraph
@@ -38,50 +39,91 @@ def main():
     g = TrainStepGraph(model, crit, opt, warmup=2)
     inputs = g._prepare(*b)
     key = g._signature(inputs) + (("padding_free", True),)
-    # capture exactly as TrainStepGraph._capture, with the debug mode on
+    # capture exactly as TrainStepGraph._capture, keeping the hipGraph_t
     orig_graph = torch.cuda.CUDAGraph
-
-    class DebugGraph(orig_graph):
-        def __init__(self, *x, **k):
-            super().__init__(*x, **k)
-            self.enable_debug_mode()
     import gdino_amd.stepgraph as sg
-    sg.torch.cuda.CUDAGraph = DebugGraph
+    sg.torch.cuda.CUDAGraph = lambda: orig_graph(keep_graph=True)
     try:
         c = g._capture(key, inputs, True)
     finally:
         sg.torch.cuda.CUDAGraph = orig_graph
     torch.cuda.synchronize()
-    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
-    c.graph.debug_dump(a.out)
-    txt = open(a.out).read()
-    kinds = collections.Counter()
-    names = collections.Counter()
-    for m in re.finditer(r'\[\s*(?:shape|style|label)[^\]]*\]', txt):
-        pass
-    for line in txt.splitlines():
-        low = line.lower()
-        if "label" not in low:
-            continue
-        if "memcpy" in low:
-            kinds["memcpy"] += 1
-            d = re.search(r"(HtoD|DtoH|DtoD|HtoH|hipMemcpy\w+)", line)
-            names["memcpy " + (d.group(1) if d else line.strip()[:120])] += 1
-        elif "memset" in low:
-            kinds["memset"] += 1
-            names["memset " + line.strip()[:160]] += 1
-        elif "host" in low and "kernel" not in low:
-            kinds["host"] += 1
-            names["host " + line.strip()[:160]] += 1
-        elif "event" in low:
-            kinds["event"] += 1
-            names["event " + line.strip()[:160]] += 1
-        elif "kernel" in low or "func" in low:
-            kinds["kernel"] += 1
-    print("graph nodes by kind:", dict(kinds), flush=True)
-    for k, v in names.most_common(60):
-        print(f"{v:5d}  {k}")
-    print(f"dot: {a.out} ({len(txt) / 1e6:.1f} MB)")
+    analyse(c.graph.raw_cuda_graph(), a.out)
+
+
+_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "child_graph", 5: "empty", 6: "wait_event",
+          7: "event_record", 8: "ext_sem_signal", 9: "ext_sem_wait", 10: "mem_alloc", 11: "mem_free",
+          12: "memcpy_from_symbol", 13: "memcpy_to_symbol"}
+
+
+class _Dim3(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint), ("y", ctypes.c_uint), ("z", ctypes.c_uint)]
+
+
+class _KParams(ctypes.Structure):  # hipKernelNodeParams
+    _fields_ = [("blockDim", _Dim3), ("extra", ctypes.c_void_p), ("func", ctypes.c_void_p), ("gridDim", _Dim3),
+                ("kernelParams", ctypes.c_void_p), ("sharedMemBytes", ctypes.c_uint)]
+
+
+def analyse(graph, out):
+    """Node types, kernel names, and the graph's shape: a single stream's
+    capture is a chain; a node with several predecessors / successors is a
+    fork / join -- work a replay may run concurrently."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    gp = ctypes.c_void_p(graph)
+    n = ctypes.c_size_t(0)
+    assert hip.hipGraphGetNodes(gp, None, ctypes.byref(n)) == 0
+    nodes = (ctypes.c_void_p * n.value)()
+    assert hip.hipGraphGetNodes(gp, nodes, ctypes.byref(n)) == 0
+    ne = ctypes.c_size_t(0)
+    assert hip.hipGraphGetEdges(gp, None, None, ctypes.byref(ne)) == 0
+    fr = (ctypes.c_void_p * max(ne.value, 1))()
+    to = (ctypes.c_void_p * max(ne.value, 1))()
+    assert hip.hipGraphGetEdges(gp, fr, to, ctypes.byref(ne)) == 0
+    hip.hipKernelNameRefByPtr.restype = ctypes.c_char_p
+    hip.hipKernelNameRefByPtr.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    kinds, names, info = collections.Counter(), collections.Counter(), {}
+    for nd in nodes:
+        t = ctypes.c_int(-1)
+        hip.hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(t))
+        kind = _TYPES.get(t.value, str(t.value))
+        kinds[kind] += 1
+        label = kind
+        if t.value == 0:
+            kp = _KParams()
+            if hip.hipGraphKernelNodeGetParams(ctypes.c_void_p(nd), ctypes.byref(kp)) == 0 and kp.func:
+                nm = hip.hipKernelNameRefByPtr(ctypes.c_void_p(kp.func), None)
+                label = (nm.decode(errors="replace") if nm else "?")[:110]
+        info[nd] = label
+        if t.value != 0:
+            names[label] += 1
+    indeg, outdeg = collections.Counter(), collections.Counter()
+    succ = collections.defaultdict(list)
+    for i in range(ne.value):
+        outdeg[fr[i]] += 1
+        indeg[to[i]] += 1
+        succ[fr[i]].append(to[i])
+    forks = [nd for nd in nodes if outdeg[nd] > 1]
+    joins = [nd for nd in nodes if indeg[nd] > 1]
+    roots = [nd for nd in nodes if indeg[nd] == 0]
+    lines = [f"nodes {n.value} edges {ne.value} roots {len(roots)} forks {len(forks)} joins {len(joins)}",
+             "by kind: " + json.dumps(dict(kinds))]
+    for k, v in names.most_common():
+        lines.append(f"  non-kernel node {k}: {v}")
+    for nd in forks[:40]:
+        lines.append("FORK " + info[nd] + " -> " + " | ".join(info[x] for x in succ[nd]))
+    for nd in joins[:40]:
+        lines.append(f"JOIN (in {indeg[nd]}) " + info[nd])
+    for nd in roots[:10]:
+        lines.append("ROOT " + info[nd])
+    txt = "\n".join(lines)
+    print(txt, flush=True)
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    with open(out, "w") as f:
+        f.write(txt + "\n")
+        order = list(nodes)
+        for nd in order:
+            f.write(f"{info[nd]}  in={indeg[nd]} out={outdeg[nd]}\n")
 
 
 if __name__ == "__main__":

@@ -17,8 +17,13 @@ the probed data: a reordering shows as a nonzero count, never as a fault.
 import argparse
 import ctypes
 import json
+import os
+import sys
 
 import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
 
 def main():
@@ -80,6 +85,38 @@ def main():
     synced = (int(bad_set), int(bad_cpy))
     print(json.dumps({"eager_bad": eager, "replays": a.replays, "back_to_back_bad(memset, memcpy)": back,
                       "synced_bad(memset, memcpy)": synced}), flush=True)
+    sort_probe(a.replays // 10)
+
+
+def sort_probe(replays):
+    """misc.topk_indices' capture path (a stable descending sort + slice) as
+    a graph: on new scores each replay must return what eager topk returns
+    (indices in range, same set).  The indices are only compared, never
+    used to address memory."""
+    from gdino_amd.misc import topk_indices
+    dev = torch.device("cuda")
+    res = {}
+    for n, k in ((2550, 300), (22223, 900)):
+        x = torch.randn(2, n, device=dev)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            topk_indices(x, k)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            idx = topk_indices(x, k)
+        bad_range = bad_set = 0
+        for i in range(replays):
+            x.copy_(torch.randn(2, n, device=dev))
+            g.replay()
+            torch.cuda.synchronize()
+            got = idx.clone()
+            bad_range += int(((got < 0) | (got >= n)).sum())
+            ref = torch.topk(x, k, dim=1)[1]
+            bad_set += int((got.sort(1)[0] != ref.sort(1)[0]).sum())
+        res[f"{n}/{k}"] = {"out_of_range": bad_range, "set_mismatch": bad_set}
+    print(json.dumps({"sort_probe": res, "replays": replays}), flush=True)
 
 
 if __name__ == "__main__":
