@@ -65,6 +65,61 @@ class _KParams(ctypes.Structure):  # hipKernelNodeParams
                 ("kernelParams", ctypes.c_void_p), ("sharedMemBytes", ctypes.c_uint)]
 
 
+class _Pos(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_size_t), ("y", ctypes.c_size_t), ("z", ctypes.c_size_t)]
+
+
+class _PPtr(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("pitch", ctypes.c_size_t), ("xsize", ctypes.c_size_t),
+                ("ysize", ctypes.c_size_t)]
+
+
+class _Ext(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_size_t), ("height", ctypes.c_size_t), ("depth", ctypes.c_size_t)]
+
+
+class _M3D(ctypes.Structure):  # hipMemcpy3DParms
+    _fields_ = [("srcArray", ctypes.c_void_p), ("srcPos", _Pos), ("srcPtr", _PPtr), ("dstArray", ctypes.c_void_p),
+                ("dstPos", _Pos), ("dstPtr", _PPtr), ("extent", _Ext), ("kind", ctypes.c_int)]
+
+
+class _MSet(ctypes.Structure):  # hipMemsetParams
+    _fields_ = [("dst", ctypes.c_void_p), ("pitch", ctypes.c_size_t), ("value", ctypes.c_uint),
+                ("elementSize", ctypes.c_uint), ("width", ctypes.c_size_t), ("height", ctypes.c_size_t)]
+
+
+class _PAttr(ctypes.Structure):  # hipPointerAttribute_t (leading fields)
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+def _ptr_kind(hip, p):
+    a = _PAttr()
+    r = hip.hipPointerGetAttributes(ctypes.byref(a), ctypes.c_void_p(p))
+    if r != 0:
+        hip.hipGetLastError()
+        return "unregistered-host"
+    return {0: "unregistered", 1: "host", 2: "device", 3: "managed"}.get(a.type, str(a.type))
+
+
+def _memcpy_desc(hip, nd):
+    m = _M3D()
+    if hip.hipGraphMemcpyNodeGetParams(ctypes.c_void_p(nd), ctypes.byref(m)) != 0:
+        hip.hipGetLastError()
+        return "(params?)"
+    kind = {0: "HtoH", 1: "HtoD", 2: "DtoH", 3: "DtoD", 4: "default"}.get(m.kind, str(m.kind))
+    nbytes = m.extent.width * max(m.extent.height, 1) * max(m.extent.depth, 1)
+    return (f"{kind} {nbytes} B src={_ptr_kind(hip, m.srcPtr.ptr or 0)} dst={_ptr_kind(hip, m.dstPtr.ptr or 0)}")
+
+
+def _memset_desc(hip, nd):
+    m = _MSet()
+    if hip.hipGraphMemsetNodeGetParams(ctypes.c_void_p(nd), ctypes.byref(m)) != 0:
+        hip.hipGetLastError()
+        return "(params?)"
+    return f"{m.width * max(m.height, 1) * m.elementSize} B value={m.value} dst={_ptr_kind(hip, m.dst or 0)}"
+
+
 def analyse(graph, out):
     """Node types, kernel names, and the graph's shape: a single stream's
     capture is a chain; a node with several predecessors / successors is a
@@ -94,6 +149,10 @@ def analyse(graph, out):
             if hip.hipGraphKernelNodeGetParams(ctypes.c_void_p(nd), ctypes.byref(kp)) == 0 and kp.func:
                 nm = hip.hipKernelNameRefByPtr(ctypes.c_void_p(kp.func), None)
                 label = (nm.decode(errors="replace") if nm else "?")[:110]
+        if t.value == 1:
+            label = "memcpy " + _memcpy_desc(hip, nd)
+        elif t.value == 2:
+            label = "memset " + _memset_desc(hip, nd)
         info[nd] = label
         if t.value != 0:
             names[label] += 1
