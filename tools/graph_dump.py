@@ -49,6 +49,16 @@ def main():
         sg.torch.cuda.CUDAGraph = orig_graph
     torch.cuda.synchronize()
     analyse(c.graph.raw_cuda_graph(), a.out)
+    hip = ctypes.CDLL("libamdhip64.so")
+    dot = os.path.abspath(a.out + ".dot").encode()
+    r = hip.hipGraphDebugDotPrint(ctypes.c_void_p(c.graph.raw_cuda_graph()), ctypes.c_char_p(dot),
+                                  ctypes.c_uint(0xFFFF))  # every verbose flag
+    print(f"hipGraphDebugDotPrint -> {r}: {dot.decode()}", flush=True)
+    if r == 0 and os.path.exists(dot):
+        for line in open(dot, errors="replace"):
+            low = line.lower()
+            if ("memcpy" in low or "memset" in low) and "label" in low:
+                print("DOT", line.strip()[:400])
 
 
 _TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "child_graph", 5: "empty", 6: "wait_event",
