@@ -136,15 +136,25 @@ contrastive_v2_kernel(const T* __restrict__ x, int64_t xsb, int64_t xsq, const T
           xf[qt] = ld_frag<T>(xb + int64_t(q < Q ? q : 0) * xsq + 32 * ch + 8 * g, q < Q);
         }
       };
-      WFrag<T> tf[2][4], xf[2][QT];
-      load(0, tf[0], xf[0]);
-      for (int ch = 0; ch < nch; ++ch) {
-        const int cur = ch & 1;
-        if (ch + 1 < nch) load(ch + 1, tf[cur ^ 1], xf[cur ^ 1]);  // next chunk in flight
+      // two register sets, the loop unrolled by two so that every index
+      // into them is a compile-time constant: a runtime-indexed [2][...]
+      // fragment array is placed in scratch (private memory), and this
+      // kernel then needs a scratch allocation on every queue it runs on
+      WFrag<T> tf0[4], xf0[QT], tf1[4], xf1[QT];
+      auto mma = [&](const WFrag<T>* tf, const WFrag<T>* xf) {
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-          for (int tt = 0; tt < 4; ++tt) acc[qt][tt] = wmma(xf[cur][qt], tf[cur][tt], acc[qt][tt]);
+          for (int tt = 0; tt < 4; ++tt) acc[qt][tt] = wmma(xf[qt], tf[tt], acc[qt][tt]);
+      };
+      load(0, tf0, xf0);
+      for (int ch = 0; ch < nch; ch += 2) {
+        if (ch + 1 < nch) load(ch + 1, tf1, xf1);  // next chunk in flight
+        mma(tf0, xf0);
+        if (ch + 1 < nch) {
+          if (ch + 2 < nch) load(ch + 2, tf0, xf0);
+          mma(tf1, xf1);
+        }
       }
     }
 #pragma unroll
