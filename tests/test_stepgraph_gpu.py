@@ -167,3 +167,41 @@ def test_step_graph_captures_the_bucketed_allreduce():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "ALLREDUCE_CAPTURE_OK" in r.stdout, (r.returncode, r.stdout[-2000:],
                                                                       r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("tokens", [(300, 2), (900, 2)])
+def test_token_linear_grads_in_a_graph(relu, tokens):
+    """One decoder-FFN-shaped TokenLinear (sequence-first [Q, B, 256] ->
+    2048, bf16 autocast, split-K weight / bias gradient) captured with its
+    backward: the replayed weight and bias gradients equal the eager ones."""
+    from gdino_amd import castcache
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(256, 2048).to(DEV)
+    x0 = torch.randn(*tokens, 256, device=DEV)
+    g0 = torch.randn(*tokens, 2048, device=DEV)
+
+    def step(x):
+        lin.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = castcache.linear_relu(x, lin) if relu else castcache.linear(x, lin.weight, lin.bias)
+        (y.float() * g0).sum().backward()
+
+    step(x0)
+    torch.cuda.synchronize()
+    ref = (lin.weight.grad.clone(), lin.bias.grad.clone())
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step(x0)
+        step(x0)
+    torch.cuda.current_stream().wait_stream(side)
+    lin.zero_grad(set_to_none=True)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=side):
+        step(x0)
+    gr.replay()
+    torch.cuda.synchronize()
+    for name, a, b in (("weight", lin.weight.grad, ref[0]), ("bias", lin.bias.grad, ref[1])):
+        d = float((a - b).norm() / b.norm())
+        assert d <= 1e-5, (name, d, float(a.norm()), float(b.norm()))
