@@ -192,10 +192,13 @@ def test_token_linear_grads_in_a_graph(relu, tokens):
     ref = (lin.weight.grad.clone(), lin.bias.grad.clone())
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
+    castcache.drop_autograd_refs()  # as TrainStepGraph: no cast node of the default stream
     with torch.cuda.stream(side):
         step(x0)
         step(x0)
+    castcache.drop_autograd_refs()
     torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
     lin.zero_grad(set_to_none=True)
     gr = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gr, stream=side):
