@@ -86,6 +86,7 @@ def main():
     print(json.dumps({"eager_bad": eager, "replays": a.replays, "back_to_back_bad(memset, memcpy)": back,
                       "synced_bad(memset, memcpy)": synced}), flush=True)
     sort_probe(a.replays // 10)
+    reduce_probe(a.replays // 10)
 
 
 def sort_probe(replays):
@@ -117,6 +118,33 @@ def sort_probe(replays):
             bad_set += int((got.sort(1)[0] != ref.sort(1)[0]).sum())
         res[f"{n}/{k}"] = {"out_of_range": bad_range, "set_mismatch": bad_set}
     print(json.dumps({"sort_probe": res, "replays": replays}), flush=True)
+
+
+def reduce_probe(replays):
+    """PyTorch column sums (the bias gradient of a plain Linear: grad.sum(0))
+    inside a graph against eager: the multi-block reductions zero their
+    semaphores with a 4-byte hipMemsetAsync, a memset node in the graph."""
+    dev = torch.device("cuda")
+    res = {}
+    for shape in ((600, 2048), (1800, 2048), (600, 256), (44446, 256), (2, 22223, 256)):
+        x = torch.randn(*shape, device=dev)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            x.sum(0)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            y = x.sum(0)
+        worst = 0.0
+        for i in range(replays):
+            x.copy_(torch.randn(*shape, device=dev))
+            g.replay()
+            torch.cuda.synchronize()
+            ref = x.sum(0)
+            worst = max(worst, float((y - ref).abs().max() / ref.abs().max()))
+        res[str(shape)] = worst
+    print(json.dumps({"reduce_probe_max_rel_err": res, "replays": replays}), flush=True)
 
 
 if __name__ == "__main__":
