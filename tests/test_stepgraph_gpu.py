@@ -102,7 +102,10 @@ def _check(res):
         for n in ge:
             d, noise = rel(gg[n], ge[n]), rel(ge2[n], ge[n])
             if not d <= max(1e-3, 3 * noise):
-                bad.append((n, d, noise, float(gg[n].norm()), float(ge[n].norm())))
+                bad.append((n, d, noise, float(gg[n].norm()), float(ge[n].norm()),
+                            gg[n].reshape(-1)[:6].tolist(), ge[n].reshape(-1)[:6].tolist(),
+                            float((gg[n].double() @ ge[n].double().reshape(-1, 1).reshape(-1))
+                                  / (ge[n].double().norm() ** 2))))
         assert not bad, (len(bad), bad[:12])
 
 
@@ -208,3 +211,49 @@ def test_token_linear_grads_in_a_graph(relu, tokens):
     for name, a, b in (("weight", lin.weight.grad, ref[0]), ("bias", lin.bias.grad, ref[1])):
         d = float((a - b).norm() / b.norm())
         assert d <= 1e-5, (name, d, float(a.norm()), float(b.norm()))
+
+
+@pytest.mark.parametrize("autocast", [True, False])
+def test_decoder_ffn_grads_in_a_graph(autocast):
+    """The decoder layer's FFN sublayer (fp32 outside autocast, reference
+    transformer.py:870-875, then add + LayerNorm) captured with its
+    backward: replayed parameter gradients equal the eager ones."""
+    from gdino_amd import castcache
+    from models.GroundingDINO.transformer import DeformableTransformerDecoderLayer
+    torch.manual_seed(0)
+    layer = DeformableTransformerDecoderLayer(256, 2048, 0.0, "relu", 4, 8, 4, False, True).to(DEV)
+    x0 = torch.randn(300, 2, 256, device=DEV)
+    g0 = torch.randn(300, 2, 256, device=DEV)
+
+    def step():
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            y = layer.forward_ffn(x)
+        (y.float() * g0).sum().backward()
+
+    step()
+    torch.cuda.synchronize()
+    ref = {n: p.grad.clone() for n, p in layer.named_parameters() if p.grad is not None}
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    castcache.drop_autograd_refs()
+    with torch.cuda.stream(side):
+        step()
+        step()
+    castcache.drop_autograd_refs()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    layer.zero_grad(set_to_none=True)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=side):
+        step()
+    gr.replay()
+    torch.cuda.synchronize()
+    bad = []
+    for n, p in layer.named_parameters():
+        if n in ref:
+            d = float((p.grad - ref[n]).norm() / ref[n].norm().clamp_min(1e-30))
+            if d > 1e-5:
+                bad.append((n, d, p.grad.reshape(-1)[:3].tolist(), ref[n].reshape(-1)[:3].tolist()))
+    assert not bad, bad
