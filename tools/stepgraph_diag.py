@@ -1,0 +1,62 @@
+"""Which part of the captured train step makes a replayed gradient differ
+from the eager step's?  The step-graph test's model and batch (lr 0), eager
+vs graph, with pieces of the captured body switched off:
+
+    python tools/stepgraph_diag.py [--clip 0|1] [--opt 0|1] [--full]
+
+Prints the parameters whose replayed gradient differs (relative norm > 1e-3)
+and, for each, the first values of both.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "open-groundingdino_amd")]
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clip", type=int, default=1)
+    ap.add_argument("--opt", type=int, default=1)
+    ap.add_argument("--ckpt", type=int, default=0)
+    ap.add_argument("--full", action="store_true")
+    ap.add_argument("--replays", type=int, default=1)
+    a = ap.parse_args()
+    import test_stepgraph_gpu as T
+    from gdino_amd.stepgraph import TrainStepGraph
+    from gdino_amd.train import train_step
+    T.CKPT[0] = bool(a.ckpt)
+    b1 = T._batch(11, 5)
+    res = {}
+    for mode in ("eager", "graph"):
+        model, crit, opt = T._model()
+        for g in opt.param_groups:
+            g["lr"], g["weight_decay"] = 0.0, 0.0
+        if mode == "eager":
+            if not a.opt:
+                opt.step = lambda *x, **k: None
+            train_step(model, crit, opt, *b1, clip_max_norm=0.1 if a.clip else 0.0)
+        else:
+            g = TrainStepGraph(model, crit, opt, clip_max_norm=0.1 if a.clip else 0.0, warmup=2)
+            if not a.opt:
+                opt.step = lambda *x, **k: None
+            for _ in range(a.replays):
+                g(*b1)
+        torch.cuda.synchronize()
+        res[mode] = T._grads(model)
+    bad = []
+    for n, ge in res["eager"].items():
+        gg = res["graph"][n]
+        d = float((gg - ge).norm() / ge.norm().clamp_min(1e-30))
+        if d > 1e-3:
+            bad.append((n, d, gg.reshape(-1)[:4].tolist(), ge.reshape(-1)[:4].tolist()))
+    print(f"clip={a.clip} opt={a.opt} ckpt={a.ckpt}: {len(bad)} of {len(res['eager'])} gradients differ", flush=True)
+    for row in bad[:20]:
+        print("  ", row, flush=True)
+
+
+if __name__ == "__main__":
+    main()
