@@ -51,9 +51,9 @@ def main():
     for n, ge in res["eager"].items():
         gg = res["graph"][n]
         d = float((gg - ge).norm() / ge.norm().clamp_min(1e-30))
-        if d > 1e-3:
+        if d > 0.05:
             bad.append((n, d, gg.reshape(-1)[:4].tolist(), ge.reshape(-1)[:4].tolist()))
-    print(f"clip={a.clip} opt={a.opt} ckpt={a.ckpt}: {len(bad)} of {len(res['eager'])} gradients differ", flush=True)
+    print(f"clip={a.clip} opt={a.opt} ckpt={a.ckpt}: {len(bad)} of {len(res['eager'])} gradients differ by > 5%", flush=True)
     for row in bad[:20]:
         print("  ", row, flush=True)
 
