@@ -24,14 +24,16 @@ def main():
     ap.add_argument("--ckpt", type=int, default=0)
     ap.add_argument("--full", action="store_true")
     ap.add_argument("--replays", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=2, help="1: 5 targets (the capture batch), 2: 3 targets")
     a = ap.parse_args()
     import test_stepgraph_gpu as T
     from gdino_amd.stepgraph import TrainStepGraph
     from gdino_amd.train import train_step
     T.CKPT[0] = bool(a.ckpt)
-    b1 = T._batch(11, 5)
+    b1 = T._batch(11, 5) if a.batch == 1 else T._batch(12, 3)
+    b0 = T._batch(11, 5)  # the capture batch (the test captures on 5 targets, replays 3)
     res = {}
-    for mode in ("eager", "graph"):
+    for mode in ("eager", "body", "graph"):
         model, crit, opt = T._model()
         for g in opt.param_groups:
             g["lr"], g["weight_decay"] = 0.0, 0.0
@@ -39,23 +41,32 @@ def main():
             if not a.opt:
                 opt.step = lambda *x, **k: None
             train_step(model, crit, opt, *b1, clip_max_norm=0.1 if a.clip else 0.0)
+        elif mode == "body":  # the captured body run eagerly on the padded inputs
+            g = TrainStepGraph(model, crit, opt, clip_max_norm=0.1 if a.clip else 0.0, warmup=2)
+            if not a.opt:
+                opt.step = lambda *x, **k: None
+            opt.zero_grad(set_to_none=True)
+            g._body(g._prepare(*b1), True)
         else:
             g = TrainStepGraph(model, crit, opt, clip_max_norm=0.1 if a.clip else 0.0, warmup=2)
             if not a.opt:
                 opt.step = lambda *x, **k: None
+            g(*b0)
             for _ in range(a.replays):
                 g(*b1)
         torch.cuda.synchronize()
         res[mode] = T._grads(model)
-    bad = []
-    for n, ge in res["eager"].items():
-        gg = res["graph"][n]
-        d = float((gg - ge).norm() / ge.norm().clamp_min(1e-30))
-        if d > 0.05:
-            bad.append((n, d, gg.reshape(-1)[:4].tolist(), ge.reshape(-1)[:4].tolist()))
-    print(f"clip={a.clip} opt={a.opt} ckpt={a.ckpt}: {len(bad)} of {len(res['eager'])} gradients differ by > 5%", flush=True)
-    for row in bad[:20]:
-        print("  ", row, flush=True)
+    for other in ("body", "graph"):
+        bad = []
+        for n, ge in res["eager"].items():
+            gg = res[other][n]
+            d = float((gg - ge).norm() / ge.norm().clamp_min(1e-30))
+            if d > 0.05:
+                bad.append((n, d, gg.reshape(-1)[:4].tolist(), ge.reshape(-1)[:4].tolist()))
+        print(f"batch={a.batch} clip={a.clip} opt={a.opt} ckpt={a.ckpt} {other} vs eager: {len(bad)} of "
+              f"{len(res['eager'])} gradients differ by > 5%", flush=True)
+        for row in bad[:10]:
+            print("  ", row, flush=True)
 
 
 if __name__ == "__main__":
