@@ -95,7 +95,7 @@ def _check(res):
     to bf16, index_add) change summation orders between any two runs"""
     def rel(a, b):
         return float((a - b).norm() / b.norm().clamp_min(1e-30))
-    for (le, ge), (le2, ge2), (lg, gg) in zip(res["eager"], res["eager2"], res["graph"]):
+    for bi, ((le, ge), (le2, ge2), (lg, gg)) in enumerate(zip(res["eager"], res["eager2"], res["graph"])):
         assert abs(le - lg) <= max(1e-5 * abs(le), 3 * abs(le - le2)), (le, le2, lg)
         assert ge.keys() == gg.keys() and len(ge) > 100
         bad = []
@@ -106,7 +106,7 @@ def _check(res):
                             gg[n].reshape(-1)[:6].tolist(), ge[n].reshape(-1)[:6].tolist(),
                             float((gg[n].double() @ ge[n].double().reshape(-1, 1).reshape(-1))
                                   / (ge[n].double().norm() ** 2))))
-        assert not bad, (len(bad), bad[:12])
+        assert not bad, ("batch", bi, len(bad), bad[:12])
 
 
 CKPT = [True]
