@@ -33,13 +33,16 @@ def main():
     b1 = T._batch(11, 5) if a.batch == 1 else T._batch(12, 3)
     b0 = T._batch(11, 5)  # the capture batch (the test captures on 5 targets, replays 3)
     res = {}
-    for mode in ("eager", "body", "graph"):
+    for mode in ("eager", "eager_seq", "body", "graph"):
         model, crit, opt = T._model()
         for g in opt.param_groups:
             g["lr"], g["weight_decay"] = 0.0, 0.0
         if mode == "eager":
             if not a.opt:
                 opt.step = lambda *x, **k: None
+            train_step(model, crit, opt, *b1, clip_max_norm=0.1 if a.clip else 0.0)
+        elif mode == "eager_seq":  # the test's order: the capture batch first, then this one
+            train_step(model, crit, opt, *b0, clip_max_norm=0.1 if a.clip else 0.0)
             train_step(model, crit, opt, *b1, clip_max_norm=0.1 if a.clip else 0.0)
         elif mode == "body":  # the captured body run eagerly on the padded inputs
             g = TrainStepGraph(model, crit, opt, clip_max_norm=0.1 if a.clip else 0.0, warmup=2)
@@ -56,7 +59,7 @@ def main():
                 g(*b1)
         torch.cuda.synchronize()
         res[mode] = T._grads(model)
-    for other in ("body", "graph"):
+    for other in ("eager_seq", "body", "graph"):
         bad = []
         for n, ge in res["eager"].items():
             gg = res[other][n]
