@@ -72,5 +72,52 @@ def main():
             print("  ", row, flush=True)
 
 
+
+
+def test_flow(skip_eager=False, grads_between=True, fresh=False):
+    """tests/test_stepgraph_gpu._run's exact order; -> {param: relative
+    difference} for the second batch (graph vs the eager reference)."""
+    import test_stepgraph_gpu as T
+    from gdino_amd.stepgraph import TrainStepGraph
+    from gdino_amd.train import train_step
+    b1, b2 = T._batch(11, 5), T._batch(12, 3)
+    out = {}
+    modes = ("graph", "eager") if skip_eager else ("eager", "eager2", "graph")
+    for mode in modes:
+        model, crit, opt = T._model()
+        for g in opt.param_groups:
+            g["lr"], g["weight_decay"] = 0.0, 0.0
+        grads = []
+        if mode.startswith("eager"):
+            for b in (b1, b2):
+                train_step(model, crit, opt, *b)
+                grads.append(T._grads(model))
+        else:
+            g = TrainStepGraph(model, crit, opt, warmup=2)
+            for b in ((T._batch(11, 5), T._batch(12, 3)) if fresh else (b1, b2)):
+                float(g(*b))
+                if grads_between or b is b2:
+                    grads.append(T._grads(model))
+            if not grads_between:
+                grads.insert(0, None)
+        torch.cuda.synchronize()
+        out[mode] = grads
+    res = {}
+    for n, ge in out["eager"][1].items():
+        gg = out["graph"][1][n]
+        res[n] = float((gg - ge).norm() / ge.norm().clamp_min(1e-30))
+    return res
+
+
+def flows():
+    for kw in ({}, {"skip_eager": True}, {"grads_between": False}, {"fresh": True}):
+        res = test_flow(**kw)
+        bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
+        print(f"flow {kw}: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--flows" in sys.argv:
+        flows()
+    else:
+        main()
