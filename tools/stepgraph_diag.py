@@ -119,5 +119,54 @@ def flows():
 if __name__ == "__main__":
     if "--flows" in sys.argv:
         flows()
+    elif "--pools" in sys.argv:
+        pools()
     else:
         main()
+
+
+def pools():
+    """After the first replay: which memory pool holds each parameter's
+    .grad (the graph's private pool or the regular one), and which grads
+    were not None when the capture began."""
+    import test_stepgraph_gpu as T
+    from gdino_amd import stepgraph
+    from gdino_amd.stepgraph import TrainStepGraph
+    model, crit, opt = T._model()
+    for g in opt.param_groups:
+        g["lr"], g["weight_decay"] = 0.0, 0.0
+    names = {id(p): n for n, p in model.named_parameters()}
+    orig = torch.cuda.graph.__enter__
+    seen = {}
+
+    def enter(self):
+        seen["not_none"] = [names.get(id(p), "?") for p in model.parameters() if p.grad is not None]
+        return orig(self)
+    torch.cuda.graph.__enter__ = enter
+    try:
+        g = TrainStepGraph(model, crit, opt, warmup=2)
+        g(*T._batch(11, 5))
+    finally:
+        torch.cuda.graph.__enter__ = orig
+    torch.cuda.synchronize()
+    segs = torch.cuda.memory_snapshot()
+    ranges = [(s["address"], s["address"] + s["total_size"], tuple(s.get("segment_pool_id", (0, 0)))) for s in segs]
+
+    def pool_of(ptr):
+        for lo, hi, pid in ranges:
+            if lo <= ptr < hi:
+                return pid
+        return None
+    by_pool = {}
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            by_pool.setdefault("none", []).append(n)
+            continue
+        by_pool.setdefault(str(pool_of(p.grad.data_ptr())), []).append(n)
+    print("grads not None at capture begin:", seen.get("not_none", [])[:10], flush=True)
+    for k, v in by_pool.items():
+        print(f"pool {k}: {len(v)} grads, e.g. {v[:3]}", flush=True)
+    for n in ("transformer.decoder.layers.0.linear1.bias", "transformer.decoder.layers.0.linear1.weight"):
+        p = dict(model.named_parameters())[n]
+        print(n, "grad pool", pool_of(p.grad.data_ptr()), "is view", p.grad._base is not None,
+              "dtype", p.grad.dtype, "stride", p.grad.stride(), flush=True)
