@@ -116,14 +116,6 @@ def flows():
         print(f"flow {kw}: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
 
 
-if __name__ == "__main__":
-    if "--flows" in sys.argv:
-        flows()
-    elif "--pools" in sys.argv:
-        pools()
-    else:
-        main()
-
 
 def pools():
     """After the first replay: which memory pool holds each parameter's
@@ -170,3 +162,12 @@ def pools():
         p = dict(model.named_parameters())[n]
         print(n, "grad pool", pool_of(p.grad.data_ptr()), "is view", p.grad._base is not None,
               "dtype", p.grad.dtype, "stride", p.grad.stride(), flush=True)
+
+
+if __name__ == "__main__":
+    if "--flows" in sys.argv:
+        flows()
+    elif "--pools" in sys.argv:
+        pools()
+    else:
+        main()
