@@ -74,7 +74,7 @@ def main():
 
 
 
-def test_flow(skip_eager=False, grads_between=True, fresh=False):
+def test_flow(skip_eager=False, grads_between=True, fresh=False, between=None):
     """tests/test_stepgraph_gpu._run's exact order; -> {param: relative
     difference} for the second batch (graph vs the eager reference)."""
     import test_stepgraph_gpu as T
@@ -96,7 +96,10 @@ def test_flow(skip_eager=False, grads_between=True, fresh=False):
             g = TrainStepGraph(model, crit, opt, warmup=2)
             for b in ((T._batch(11, 5), T._batch(12, 3)) if fresh else (b1, b2)):
                 float(g(*b))
-                if grads_between or b is b2:
+                if b is not b2 and between is not None:
+                    keep = between(model)  # noqa: F841  (held across the next replay)
+                    grads.append(None)
+                elif grads_between or b is b2:
                     grads.append(T._grads(model))
             if not grads_between:
                 grads.insert(0, None)
@@ -110,9 +113,24 @@ def test_flow(skip_eager=False, grads_between=True, fresh=False):
 
 
 def flows():
-    for kw in ({}, {"skip_eager": True}, {"grads_between": False}, {"fresh": True}):
+    def big(model):
+        return torch.empty(int(700e6) // 4, device="cuda")
+
+    def norms(model):
+        return [float(p.grad.norm()) for p in model.parameters() if p.grad is not None]
+
+    def clones_freed(model):
+        T_grads = [p.grad.clone() for p in model.parameters() if p.grad is not None]
+        del T_grads
+        return None
+
+    import test_stepgraph_gpu as T
+    for kw in ({"skip_eager": True}, {"skip_eager": True, "between": big},
+               {"skip_eager": True, "between": norms}, {"skip_eager": True, "between": clones_freed},
+               {"skip_eager": True, "between": T._grads}):
         res = test_flow(**kw)
         bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
+        kw = {k: getattr(v, "__name__", v) for k, v in kw.items()}
         print(f"flow {kw}: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
 
 
