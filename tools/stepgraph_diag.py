@@ -124,10 +124,33 @@ def flows():
         del T_grads
         return None
 
-    import test_stepgraph_gpu as T
-    for kw in ({"skip_eager": True}, {"skip_eager": True, "between": big},
-               {"skip_eager": True, "between": norms}, {"skip_eager": True, "between": clones_freed},
-               {"skip_eager": True, "between": T._grads}):
+    def clone_named(pred):
+        def f(model):
+            keep = [p.grad.clone() for n, p in model.named_parameters() if p.grad is not None and pred(n, p)]
+            return keep
+        f.__name__ = pred.__name__
+        return f
+
+    def only_dec0_lin1_bias(n, p):
+        return n == "transformer.decoder.layers.0.linear1.bias"
+
+    def only_biases(n, p):
+        return n.endswith("bias")
+
+    def no_biases(n, p):
+        return not n.endswith("bias")
+
+    def small(n, p):
+        return p.numel() * 4 < (1 << 20)
+
+    def dec_only(n, p):
+        return ".decoder." in n
+
+    for kw in ({"skip_eager": True, "between": clone_named(only_dec0_lin1_bias)},
+               {"skip_eager": True, "between": clone_named(only_biases)},
+               {"skip_eager": True, "between": clone_named(no_biases)},
+               {"skip_eager": True, "between": clone_named(small)},
+               {"skip_eager": True, "between": clone_named(dec_only)}):
         res = test_flow(**kw)
         bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
         kw = {k: getattr(v, "__name__", v) for k, v in kw.items()}
