@@ -210,5 +210,54 @@ if __name__ == "__main__":
         flows()
     elif "--pools" in sys.argv:
         pools()
+    elif "--history" in sys.argv:
+        history()
     else:
         main()
+
+
+def history():
+    """Allocations made while the step graph was being captured that did NOT
+    come from the graph's private pool (a capture allocates from the private
+    pool only on the capturing stream): their blocks return to the regular
+    pool when freed, and a later eager allocation can take memory the
+    replays still read or write."""
+    import collections
+    import test_stepgraph_gpu as T
+    from gdino_amd.stepgraph import TrainStepGraph
+    model, crit, opt = T._model()
+    for g in opt.param_groups:
+        g["lr"], g["weight_decay"] = 0.0, 0.0
+    torch.cuda.memory._record_memory_history(max_entries=400000)
+    marks = {}
+    orig_enter, orig_exit = torch.cuda.graph.__enter__, torch.cuda.graph.__exit__
+
+    def count():
+        return len(torch.cuda.memory._snapshot()["device_traces"][0])
+
+    def enter(self):
+        r = orig_enter(self)
+        marks["begin"] = count()
+        marks["stream"] = torch.cuda.current_stream().cuda_stream
+        return r
+
+    def exit_(self, *x):
+        marks["end"] = count()
+        return orig_exit(self, *x)
+    torch.cuda.graph.__enter__, torch.cuda.graph.__exit__ = enter, exit_
+    try:
+        g = TrainStepGraph(model, crit, opt, warmup=2)
+        g(*T._batch(11, 5))
+    finally:
+        torch.cuda.graph.__enter__, torch.cuda.graph.__exit__ = orig_enter, orig_exit
+    snap = torch.cuda.memory._snapshot()
+    torch.cuda.memory._record_memory_history(enabled=None)
+    tr = snap["device_traces"][0][marks["begin"]:marks["end"]]
+    streams = collections.Counter((e["action"], e.get("stream")) for e in tr)
+    print("capture stream", marks["stream"], "trace events by (action, stream):", dict(streams), flush=True)
+    odd = [e for e in tr if e["action"] == "alloc" and e.get("stream") != marks["stream"]]
+    print(f"{len(odd)} allocations during capture on another stream", flush=True)
+    for e in odd[:12]:
+        frames = [f"{f['filename'].split('/')[-1]}:{f['line']} {f['name']}" for f in e.get("frames", [])
+                  if "site-packages/torch" not in f["filename"] or "autograd" in f["filename"]][:6]
+        print("  size", e["size"], "stream", e.get("stream"), frames, flush=True)
