@@ -205,17 +205,6 @@ def pools():
               "dtype", p.grad.dtype, "stride", p.grad.stride(), flush=True)
 
 
-if __name__ == "__main__":
-    if "--flows" in sys.argv:
-        flows()
-    elif "--pools" in sys.argv:
-        pools()
-    elif "--history" in sys.argv:
-        history()
-    else:
-        main()
-
-
 def history():
     """Allocations made while the step graph was being captured that did NOT
     come from the graph's private pool (a capture allocates from the private
@@ -261,3 +250,15 @@ def history():
         frames = [f"{f['filename'].split('/')[-1]}:{f['line']} {f['name']}" for f in e.get("frames", [])
                   if "site-packages/torch" not in f["filename"] or "autograd" in f["filename"]][:6]
         print("  size", e["size"], "stream", e.get("stream"), frames, flush=True)
+
+
+
+if __name__ == "__main__":
+    if "--flows" in sys.argv:
+        flows()
+    elif "--pools" in sys.argv:
+        pools()
+    elif "--history" in sys.argv:
+        history()
+    else:
+        main()
