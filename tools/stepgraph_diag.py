@@ -239,9 +239,28 @@ def history():
         g(*T._batch(11, 5))
     finally:
         torch.cuda.graph.__enter__, torch.cuda.graph.__exit__ = orig_enter, orig_exit
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
     snap = torch.cuda.memory._snapshot()
     torch.cuda.memory._record_memory_history(enabled=None)
-    tr = snap["device_traces"][0][marks["begin"]:marks["end"]]
+    allt = snap["device_traces"][0]
+    # blocks allocated before the capture began and freed after it ended
+    # (what a replay may still use while an eager allocation takes it)
+    born = {}
+    for e in allt[:marks["begin"]]:
+        if e["action"] == "alloc":
+            born[e["addr"]] = e
+        elif e["action"] == "free_completed":
+            born.pop(e["addr"], None)
+    late = [e for e in allt[marks["end"]:] if e["action"] == "free_requested" and e["addr"] in born]
+    print(f"{len(late)} blocks allocated before the capture and freed after it", flush=True)
+    for e in late[:25]:
+        a = born[e["addr"]]
+        frames = [f"{f['filename'].split('/')[-1]}:{f['line']} {f['name']}" for f in a.get("frames", [])
+                  if "site-packages/torch" not in f["filename"]][:7]
+        print("  size", a["size"], frames, flush=True)
+    tr = allt[marks["begin"]:marks["end"]]
     streams = collections.Counter((e["action"], e.get("stream")) for e in tr)
     print("capture stream", marks["stream"], "trace events by (action, stream):", dict(streams), flush=True)
     odd = [e for e in tr if e["action"] == "alloc" and e.get("stream") != marks["stream"]]
