@@ -255,10 +255,10 @@ def history():
             born.pop(e["addr"], None)
     late = [e for e in allt[marks["end"]:] if e["action"] == "free_requested" and e["addr"] in born]
     print(f"{len(late)} blocks allocated before the capture and freed after it", flush=True)
-    for e in late[:25]:
+    for e in late[:40]:
         a = born[e["addr"]]
         frames = [f"{f['filename'].split('/')[-1]}:{f['line']} {f['name']}" for f in a.get("frames", [])
-                  if "site-packages/torch" not in f["filename"]][:7]
+                  if f["filename"].endswith(".py") and "site-packages" not in f["filename"]][:6]
         print("  size", a["size"], frames, flush=True)
     tr = allt[marks["begin"]:marks["end"]]
     streams = collections.Counter((e["action"], e.get("stream")) for e in tr)
