@@ -146,6 +146,20 @@ def flows():
     def dec_only(n, p):
         return ".decoder." in n
 
+    from gdino_amd.stepgraph import TrainStepGraph
+    orig_capture = TrainStepGraph._capture
+    stash = []
+
+    def capture_keep(self, key, inputs, *x):
+        stash.append(inputs)  # the first call's prepared (non-static) inputs stay alive
+        return orig_capture(self, key, inputs, *x)
+    TrainStepGraph._capture = capture_keep
+    try:
+        res = test_flow(skip_eager=True, between=T._grads)
+    finally:
+        TrainStepGraph._capture = orig_capture
+    bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
+    print(f"first call's inputs kept alive: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
     for kw in ({"skip_eager": True, "between": clone_named(only_dec0_lin1_bias)},
                {"skip_eager": True, "between": clone_named(only_biases)},
                {"skip_eager": True, "between": clone_named(no_biases)},
