@@ -146,6 +146,7 @@ def flows():
     def dec_only(n, p):
         return ".decoder." in n
 
+    import test_stepgraph_gpu as T
     from gdino_amd.stepgraph import TrainStepGraph
     orig_capture = TrainStepGraph._capture
     stash = []
