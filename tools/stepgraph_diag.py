@@ -161,11 +161,37 @@ def flows():
         TrainStepGraph._capture = orig_capture
     bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
     print(f"first call's inputs kept alive: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
-    for kw in ({"skip_eager": True, "between": clone_named(only_dec0_lin1_bias)},
-               {"skip_eager": True, "between": clone_named(only_biases)},
-               {"skip_eager": True, "between": clone_named(no_biases)},
-               {"skip_eager": True, "between": clone_named(small)},
-               {"skip_eager": True, "between": clone_named(dec_only)}):
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def raw_hipmalloc(model):
+        ptrs = []
+        for _ in range(8):
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(2 << 20)) == 0
+            ptrs.append(p)
+        for p in ptrs:
+            hip.hipFree(p)
+        return None
+
+    def raw_hipmalloc_keep(model):
+        ptrs = []
+        for _ in range(8):
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(2 << 20)) == 0
+            ptrs.append(p)
+        return ptrs
+
+    def small_tensors(model):
+        return [torch.empty(2048, device="cuda") for _ in range(200)]
+
+    def prewarm(model):
+        return None
+
+    for kw in ({"skip_eager": True, "between": raw_hipmalloc},
+               {"skip_eager": True, "between": raw_hipmalloc_keep},
+               {"skip_eager": True, "between": small_tensors},
+               {"skip_eager": True, "between": clone_named(only_biases)}):
         res = test_flow(**kw)
         bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
         kw = {k: getattr(v, "__name__", v) for k, v in kw.items()}
