@@ -160,7 +160,7 @@ def flows():
     finally:
         TrainStepGraph._capture = orig_capture
     bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
-    print(f"first call's inputs kept alive: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
+    print(f"(reference) first call's inputs kept alive: {len(bad)} gradients differ by > 5%: {bad[:4]}", flush=True)
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
 
@@ -188,10 +188,26 @@ def flows():
     def prewarm(model):
         return None
 
-    for kw in ({"skip_eager": True, "between": raw_hipmalloc},
-               {"skip_eager": True, "between": raw_hipmalloc_keep},
-               {"skip_eager": True, "between": small_tensors},
-               {"skip_eager": True, "between": clone_named(only_biases)}):
+    src = [torch.randn(2048, device="cuda") for _ in range(200)]
+    dst = [torch.empty(2048, device="cuda") for _ in range(200)]
+
+    def memcpy_d2d(model):  # contiguous same-dtype copy_: hipMemcpyAsync
+        for a_, b_ in zip(dst, src):
+            a_.copy_(b_)
+        return None
+
+    def kernel_copies(model):  # strided source: an elementwise copy kernel
+        for a_, b_ in zip(dst, src):
+            a_.view(2, 1024).copy_(b_.view(1024, 2).t())
+        return None
+
+    def one_memcpy(model):
+        dst[0].copy_(src[0])
+        return None
+
+    for kw in ({"skip_eager": True, "between": memcpy_d2d},
+               {"skip_eager": True, "between": kernel_copies},
+               {"skip_eager": True, "between": one_memcpy}):
         res = test_flow(**kw)
         bad = sorted(((d, n) for n, d in res.items() if d > 0.05), reverse=True)
         kw = {k: getattr(v, "__name__", v) for k, v in kw.items()}
