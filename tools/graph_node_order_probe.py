@@ -83,8 +83,22 @@ def main():
         g.replay()
         torch.cuda.synchronize()
     synced = (int(bad_set), int(bad_cpy))
+    # eager D2D memcpys between the replays (what corrupted the step graph)
+    bad_set.zero_()
+    bad_cpy.zero_()
+    srcs = [torch.randn(4096, device=dev) for _ in range(64)]
+    dsts = [torch.empty(4096, device=dev) for _ in range(64)]
+    for i in range(a.replays // 10):
+        g.replay()
+        torch.cuda.synchronize()
+        for _ in range(5):
+            for d_, s_ in zip(dsts, srcs):
+                d_.copy_(s_)
+        torch.cuda.synchronize()
+    interleaved = (int(bad_set), int(bad_cpy))
     print(json.dumps({"eager_bad": eager, "replays": a.replays, "back_to_back_bad(memset, memcpy)": back,
-                      "synced_bad(memset, memcpy)": synced}), flush=True)
+                      "synced_bad(memset, memcpy)": synced,
+                      "eager_memcpys_between_bad(memset, memcpy)": interleaved}), flush=True)
     sort_probe(a.replays // 10)
     reduce_probe(a.replays // 10)
 
