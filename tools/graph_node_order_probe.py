@@ -99,8 +99,52 @@ def main():
     print(json.dumps({"eager_bad": eager, "replays": a.replays, "back_to_back_bad(memset, memcpy)": back,
                       "synced_bad(memset, memcpy)": synced,
                       "eager_memcpys_between_bad(memset, memcpy)": interleaved}), flush=True)
+    small_memcpy_probe(a.replays // 10)
     sort_probe(a.replays // 10)
     reduce_probe(a.replays // 10)
+
+
+def small_memcpy_probe(replays):
+    """Small memcpy nodes (the step graph's are 4 B .. 5 MB) with eager
+    small D2D copies issued between the replays."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    dev = torch.device("cuda")
+    res = {}
+    for nbytes in (4, 1024, 8192, 614400):
+        n = nbytes // 4
+        A = torch.empty(n, device=dev)
+        B = torch.empty(n, device=dev)
+        step = torch.zeros((), device=dev)
+        bad = torch.zeros((), dtype=torch.int64, device=dev)
+
+        def body():
+            s = torch.cuda.current_stream().cuda_stream
+            A.copy_(step.expand_as(A))
+            assert hip.hipMemcpyAsync(B.data_ptr(), A.data_ptr(), nbytes, 3, s) == 0
+            bad.add_((B != step).sum())
+            step.add_(1.0)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            body()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        bad.zero_()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            body()
+        srcs = [torch.randn(2048, device=dev) for _ in range(64)]
+        dsts = [torch.empty(2048, device=dev) for _ in range(64)]
+        for i in range(replays):
+            g.replay()
+            torch.cuda.synchronize()
+            for _ in range(5):
+                for d_, s_ in zip(dsts, srcs):
+                    d_.copy_(s_)
+            torch.cuda.synchronize()
+        res[nbytes] = int(bad)
+    print(json.dumps({"small_memcpy_nodes_bad_with_eager_copies_between": res, "replays": replays}), flush=True)
 
 
 def sort_probe(replays):
