@@ -71,6 +71,10 @@
  *                        BiAttention fusion block (fuse_modules.py:285-286)
  *                        and `x = shortcut + drop_path(x)` of the Swin blocks
  *                        (swin_transformer.py:295-296) and their backward
+ *   gd_graph_memsets_to_kernels
+ *                     <- no reference counterpart: the step graph's memset
+ *                        nodes as kernel nodes (PyTorch's reductions zero
+ *                        their semaphores with a memset)
  *   gd_contrastive_forward
  *                     <- ContrastiveEmbed.forward (x . text^T, -inf on padded
  *                        tokens, -inf right padding to max_text_len)
@@ -420,6 +424,21 @@ gd_status gd_add_scaled_backward(gd_dtype g_dtype, const void* grad_out, gd_dtyp
                                  const void* branch, const float* s, int64_t s_bstride, int s_cstride,
                                  int64_t B, int64_t N, int C, void* grad_branch, float* grad_s_bc,
                                  void* workspace, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Captured-graph surgery (the train step as one HIP graph)                  */
+/* ------------------------------------------------------------------------ */
+/*
+ * graph: a captured, not yet instantiated hipGraph_t.  Every memset node is
+ * replaced by a kernel node (the library's fill kernel, same destination,
+ * value and dependencies): on ROCm 7.0 a replayed graph's memset nodes stop
+ * taking effect once eager device-to-device copies have run between
+ * replays.  Returns the number of nodes replaced, or -1 when a memset node
+ * cannot be expressed (element size not 1 / 2 / 4, a pitched 2-D memset,
+ * or a byte count not a multiple of 4); the graph is then partly rewritten
+ * and must not be used.
+ */
+int gd_graph_memsets_to_kernels(void* graph);
 
 /* ------------------------------------------------------------------------ */
 /* Hungarian matching (matcher.py:104-110)                                   */

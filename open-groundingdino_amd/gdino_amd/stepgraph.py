@@ -27,13 +27,14 @@ Reference: the step engine_multi.py:499-564 / main.py:254-292 run eagerly.
 """
 from __future__ import annotations
 
-import torch
-
+import ctypes
 import os
 import sys
 import time
 
-from . import castcache
+import torch
+
+from . import _lib, castcache
 from .misc import no_padding
 from .train import BucketedGradSync, weighted_loss
 
@@ -61,9 +62,32 @@ def _static_like(t: torch.Tensor) -> torch.Tensor:
     return torch.empty_like(t, memory_format=torch.contiguous_format)
 
 
+_lib.register("gd_graph_memsets_to_kernels", [ctypes.c_void_p])
+
+
+def memsets_to_kernels(graph: "torch.cuda.CUDAGraph") -> int:
+    """Replace every memset node of a captured (keep_graph=True, not yet
+    instantiated) graph by a fill-kernel node (csrc/graph.hip): on ROCm 7.0
+    a replay's memset nodes stop taking effect once eager device-to-device
+    copies ran between replays (tools/graph_node_order_probe.py), and
+    PyTorch's multi-block reductions zero their semaphores with one -- the
+    train-step graph then returned wrong bias gradients after a host-side
+    gradient copy (tools/stepgraph_diag.py --flows).  -> nodes replaced."""
+    fn = _lib.lib().gd_graph_memsets_to_kernels
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
+    n = int(fn(ctypes.c_void_p(graph.raw_cuda_graph())))
+    if n < 0:
+        raise RuntimeError("gd_graph_memsets_to_kernels: a memset node of the captured graph is not expressible "
+                           "as a fill kernel")
+    return n
+
+
 class _Captured:
     def __init__(self):
-        self.graph = torch.cuda.CUDAGraph()
+        # kept un-instantiated after capture: its memset nodes are rewritten
+        # (memsets_to_kernels) before the first replay
+        self.graph = torch.cuda.CUDAGraph(keep_graph=True)
+        self.memsets_replaced = 0
         self.inputs = {}
         self.loss = None
         self.loss_dict = None
@@ -193,6 +217,9 @@ class TrainStepGraph:
         with torch.cuda.graph(c.graph, stream=side):
             c.loss, c.loss_dict = self._body(c.inputs, padding_free)
         torch.cuda.current_stream().wait_stream(side)
+        c.memsets_replaced = memsets_to_kernels(c.graph)
+        c.graph.instantiate()
+        _log(f"memset nodes replaced by fill kernels: {c.memsets_replaced}")
         _log(f"captured ({c.graph.__class__.__name__})")
         self.graphs[key] = c
         self.captures += 1

@@ -47,6 +47,7 @@ def test_python_binding_signatures_cover_header():
     import gdino_amd.kernels  # noqa: F401  (kernel modules register their signatures)
     import gdino_amd.msda  # noqa: F401
     import gdino_amd.misc  # noqa: F401
+    import gdino_amd.stepgraph  # noqa: F401
     compute = [s for s in declared_symbols()
                if s not in ("gd_last_error", "gd_runtime_info", "gd_abi_version") and not s.endswith("_bytes")]
     missing = [s for s in compute if s not in _lib._SIGNATURES]

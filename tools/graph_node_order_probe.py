@@ -96,9 +96,27 @@ def main():
                 d_.copy_(s_)
         torch.cuda.synchronize()
     interleaved = (int(bad_set), int(bad_cpy))
+    # the same with the graph's memset nodes rewritten as fill kernels
+    from gdino_amd.stepgraph import memsets_to_kernels
+    g2 = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g2, stream=side):
+        body()
+    replaced = memsets_to_kernels(g2)
+    g2.instantiate()
+    bad_set.zero_()
+    bad_cpy.zero_()
+    for i in range(a.replays // 10):
+        g2.replay()
+        torch.cuda.synchronize()
+        for _ in range(5):
+            for d_, s_ in zip(dsts, srcs):
+                d_.copy_(s_)
+        torch.cuda.synchronize()
+    rewritten = (int(bad_set), int(bad_cpy), replaced)
     print(json.dumps({"eager_bad": eager, "replays": a.replays, "back_to_back_bad(memset, memcpy)": back,
                       "synced_bad(memset, memcpy)": synced,
-                      "eager_memcpys_between_bad(memset, memcpy)": interleaved}), flush=True)
+                      "eager_memcpys_between_bad(memset, memcpy)": interleaved,
+                      "memsets_as_kernels_bad(memset, memcpy, replaced)": rewritten}), flush=True)
     small_memcpy_probe(a.replays // 10)
     sort_probe(a.replays // 10)
     reduce_probe(a.replays // 10)
