@@ -198,7 +198,10 @@ def cpu_baseline(bs, recompute=False):
     for nt in sorted({threads, 1, affinity}, reverse=True):
         torch.set_num_threads(nt)
         try:
-            res[nt] = {name: timed(inp, bwd, w, r) for name, inp, bwd, w, r in cases}
+            res[nt] = {}
+            for name, inp, bwd, w, r in cases:
+                res[nt][name] = timed(inp, bwd, w, r)
+                _progress(f"cpu baseline {nt} threads {name}: median {res[nt][name]['median_s'] * 1e3:.1f} ms")
         finally:
             torch.set_num_threads(threads)
 
@@ -271,6 +274,11 @@ def pmc_traffic(kname, bs):
     return pick(rows, key=lambda k: k["grid"])["traffic_bytes"]
 
 
+def _progress(msg):
+    """one stderr line per bench phase (a silent GPU run is taken for hung)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main(argv=None, device_type="cuda", child_script=None):
     """device_type="cpu" exists for tests/test_bench_contract.py only (the
     HIP ops are then routed to the oracle by the test); the bench itself
@@ -307,6 +315,7 @@ def main(argv=None, device_type="cuda", child_script=None):
     model.train(not a.forward_only)
     from gdino_amd.train import set_activation_checkpointing
     set_activation_checkpointing(model, a.checkpointing == "on")
+    _progress("model built")
     start_epoch = 0
     # reference main.py:339 (the cfg_odvg default: StepLR every lr_drop epochs)
     sched = torch.optim.lr_scheduler.StepLR(optimizer, args.lr_drop)
@@ -357,6 +366,7 @@ def main(argv=None, device_type="cuda", child_script=None):
         try:
             step_graph(samples, targets, captions, cats)  # capture (+ its eager warm-up steps) and one replay
             sync()
+            _progress("step graph captured and replayed once")
         except Exception as e:  # capture refused: measure the eager step instead
             step_graph.release()
             step_graph = None
@@ -372,6 +382,7 @@ def main(argv=None, device_type="cuda", child_script=None):
     sync()
     if world > 1:
         dist.barrier()
+    _progress(f"{a.warmup} warm-up steps done")
 
     # MSDA launch timing over the timed region (eager); with graphs the
     # launches are inside the replays, where ROCm refuses timing events: they
@@ -409,6 +420,7 @@ def main(argv=None, device_type="cuda", child_script=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     loss_v = float(loss)
+    _progress(f"{a.steps} timed steps done: {elapsed / a.steps * 1e3:.1f} ms/step")
 
     # one extra step, outside the timed region, with HIP events around every
     # C-ABI call: device time per HIP entry point (all kernel families, not
@@ -431,6 +443,7 @@ def main(argv=None, device_type="cuda", child_script=None):
         finally:
             _lib.call_timer = None
             msda.timer = None
+        _progress("per-entry-point timing step done")
 
     images = a.bs * world * a.steps
     value = images / elapsed
@@ -503,6 +516,7 @@ def main(argv=None, device_type="cuda", child_script=None):
         if not math.isfinite(loss_v):
             res["error"] = f"non-finite loss {loss_v}: the step diverged, the throughput is not a valid measurement"
         if not a.no_cpu_baseline and world == 1:
+            _progress("cpu baseline (host cores)")
             res["cpu_baseline"] = cpu_baseline(a.bs, recompute=a.checkpointing == "on")
         print(json.dumps(res), flush=True)
     if world > 1:
