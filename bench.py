@@ -189,13 +189,17 @@ def cpu_baseline(bs, recompute=False):
     dec = make(LEVELS_800, bs, 900, 2)
     cases = [("cfg1_fwd", cfg1, False, 5, 20), ("cfg1_fwd_bwd", cfg1, True, 5, 20),
              ("enc_fwd", enc, False, 2, 5), ("enc_fwd_bwd", enc, True, 2, 5), ("dec_fwd_bwd", dec, True, 3, 10)]
+    # the process's torch thread count is the host share this GPU gets (16 on
+    # the MI355X boxes: OMP_NUM_THREADS); the affinity mask there lists all
+    # 256 cores of the machine, and 256 threads on a 16-core share ran ~9x
+    # slower than 16 (profiles/r04b_bench.json of round 4, 4.5 min of bench)
     threads = torch.get_num_threads()
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count()
     res = {}
-    for nt in sorted({threads, 1, affinity}, reverse=True):
+    for nt in sorted({threads, 1}, reverse=True):
         torch.set_num_threads(nt)
         try:
             res[nt] = {}
