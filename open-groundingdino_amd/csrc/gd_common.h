@@ -107,6 +107,43 @@ inline hipError_t fill_u32_async(void* p, uint32_t v, size_t bytes, hipStream_t 
   return hipGetLastError();
 }
 
+
+// 16 bytes per lane from global memory straight into LDS (LDS-DMA,
+// global_load_lds_dwordx4): lane l's bytes land at the wave-uniform `dst` +
+// 16 l.  Inline asm rather than __builtin_amdgcn_global_load_lds: hipcc cannot
+// tell which ring slot a builtin DMA writes, so after one it waits vmcnt(0)
+// before every later ds_read (a multi-slot ring drains each step); an asm DMA
+// is outside its wait bookkeeping and the kernel counts vmcnt itself
+// (gd_wait_vmcnt).  M0 is written and restored in the same statement
+// (cdna_hip_programming.md, "LDS-DMA recipe").  tests/emu's host header
+// defines GD_LDS_DMA16 with a host emulation of the same data movement.
+#ifndef GD_LDS_DMA16
+namespace {
+__device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
+  const uint32_t lds_addr = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)(dst))));
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_addr)
+               : "memory");
+}
+}  // namespace
+#define GD_LDS_DMA16(src, dst) ::gd::lds_dma16((src), (dst))
+#endif
+// s_waitcnt vmcnt(N) (expcnt, lgkmcnt left open), N < 64; and a bare
+// s_barrier, which unlike __syncthreads() does not wait vmcnt(0) first
+#define gd_wait_vmcnt(N)                                                      \
+  do {                                                                        \
+    __asm__ __volatile__("" ::: "memory");                                    \
+    __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | 0x0F70);     \
+  } while (0)
+#define gd_raw_barrier()                      \
+  do {                                        \
+    __asm__ __volatile__("" ::: "memory");    \
+    __builtin_amdgcn_s_barrier();             \
+    __asm__ __volatile__("" ::: "memory");    \
+  } while (0)
 }  // namespace gd
 
 // integer tuning / A-B switch from the environment (host side)

@@ -18,6 +18,7 @@
 #include "gd_common.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace gd {
 namespace {
@@ -170,36 +171,59 @@ __device__ __forceinline__ WFrag<uint16_t> tr_frag(const uint16_t* img, int fbas
   return f;
 }
 
-// grid (ceil(I/128), ceil(O/128), batch * splits); batch b reads dy + b*bsy, x + b*bsx
-template <bool BIAS>
+// grid (ceil(I/128), ceil(O/128), batch * splits); batch b reads dy + b*bsy, x + b*bsx.
+// CH tokens per staged chunk (32 or 64): a 64-token chunk is two 32-row
+// images per operand (the swizzle depends on r & 3 and (r >> 3) & 1 only, so
+// rows 32..63 continue the same pattern), 4 x 16 B of each operand in flight
+// per thread instead of 2 and half the barriers per token.
+//
+// The grid is 1-D: workgroup h is logical tile L = xcd_remap ? remap(h) : h,
+// L = ((batch * splits + split) * gy + tile_o) * gx + tile_i.  The hardware
+// deals consecutive workgroups round-robin over the 8 XCDs (each with its own
+// L2), so with L = h every split's output tiles -- which all read the same
+// token rows of X (and of dY across tile_i) -- land on 8 different L2s and
+// each fetches those rows again from the fabric.  remap(h) gives XCD h % 8 a
+// contiguous range of L (bijective for any count: cdna_hip_programming.md
+// §5, "XCD swizzle must be bijective"), so a split's tiles share one L2.
+__device__ __forceinline__ int xcd_logical(int h, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = h % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + h / 8;
+}
+
+template <bool BIAS, int CH>
 __global__ void __launch_bounds__(256)
 wgrad_tr_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, const uint16_t* __restrict__ x,
                 int64_t ldx, int64_t bsx, int T_, int O, int I, int splits, int tokens_per_split,
-                float* __restrict__ part_w, float* __restrict__ part_b) {
-  __shared__ __attribute__((aligned(16))) uint16_t ys[2][kTrChunk * kTrTile];
-  __shared__ __attribute__((aligned(16))) uint16_t xs[2][kTrChunk * kTrTile];
+                float* __restrict__ part_w, float* __restrict__ part_b, int gx, int gy, int xcd_remap) {
+  static_assert(CH == 32 || CH == 64, "chunk of 32 or 64 tokens");
+  constexpr int NH = CH / 16;  // 16-B vectors per thread per operand per chunk
+  __shared__ __attribute__((aligned(16))) uint16_t ys[2][CH * kTrTile];
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][CH * kTrTile];
   __shared__ float bsum_s[BIAS ? 16 : 1][kTrTile];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
   const int wo = wave >> 1, wi = wave & 1;  // the wave's 64 x 64 quarter
-  const int i0 = blockIdx.x * kTrTile, o0 = blockIdx.y * kTrTile;
-  const int bz = blockIdx.z / splits, split = blockIdx.z - bz * splits;
+  const int h = blockIdx.x;
+  const int L = xcd_remap ? xcd_logical(h, int(gridDim.x)) : h;
+  const int tile_i = L % gx, tile_o = (L / gx) % gy, zz = L / (gx * gy);
+  const int i0 = tile_i * kTrTile, o0 = tile_o * kTrTile;
+  const int bz = zz / splits, split = zz - bz * splits;
   dy += bz * bsy;
   x += bz * bsx;
   const int64_t part = int64_t(bz) * splits + split;
   const int tb = split * tokens_per_split;
   const int te = min(T_, tb + tokens_per_split);
-  const bool do_bias = BIAS && blockIdx.x == 0;
+  const bool do_bias = BIAS && tile_i == 0;
 
-  // loader: vectors v = tid and tid + 256 of the chunk's 32 rows x 16 chunks
+  // loader: vectors tid + 256 h of the chunk's CH rows x 16 chunks
   const int lrow = tid >> 4, lch = tid & 15;
   const bool yok = o0 + 8 * lch < O, xok = i0 + 8 * lch < I;
   const uint16_t* yp = dy + o0 + 8 * lch;
   const uint16_t* xp = x + i0 + 8 * lch;
-  uint4 ry[2], rx[2];
+  uint4 ry[NH], rx[NH];
   auto load = [&](int t0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NH; ++h) {
       const int t = t0 + lrow + 16 * h;
       const bool in = t < te;
       ry[h] = (in && yok) ? *reinterpret_cast<const uint4*>(yp + int64_t(t) * ldy) : make_uint4(0u, 0u, 0u, 0u);
@@ -218,34 +242,37 @@ wgrad_tr_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, const
 
   if (tb < te) load(tb);
   int buf = 0;
-  for (int t0 = tb; t0 < te; t0 += kTrChunk, buf ^= 1) {
+  for (int t0 = tb; t0 < te; t0 += CH, buf ^= 1) {
     uint16_t* yb = ys[buf];
     uint16_t* xb = xs[buf];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NH; ++h) {
       *reinterpret_cast<uint4*>(yb + tr_elem(lrow + 16 * h, lch)) = ry[h];
       *reinterpret_cast<uint4*>(xb + tr_elem(lrow + 16 * h, lch)) = rx[h];
     }
     if (do_bias) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < NH; ++h) {
         bacc[0] += bf16_lo(ry[h].x); bacc[1] += bf16_hi(ry[h].x);
         bacc[2] += bf16_lo(ry[h].y); bacc[3] += bf16_hi(ry[h].y);
         bacc[4] += bf16_lo(ry[h].z); bacc[5] += bf16_hi(ry[h].z);
         bacc[6] += bf16_lo(ry[h].w); bacc[7] += bf16_hi(ry[h].w);
       }
     }
-    if (t0 + kTrChunk < te) load(t0 + kTrChunk);  // next chunk in flight during the MFMAs
+    if (t0 + CH < te) load(t0 + CH);  // next chunk in flight during the MFMAs
     __syncthreads();  // image `buf` complete (and `buf ^ 1` consumed one iteration ago)
-    WFrag<uint16_t> af[4], bfr[4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) af[m] = tr_frag(yb, 64 * wo + 16 * m, lane);
+    for (int k = 0; k < CH / 32; ++k) {  // 32-token sub-images
+      WFrag<uint16_t> af[4], bfr[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(xb, 64 * wi + 16 * n, lane);
+      for (int m = 0; m < 4; ++m) af[m] = tr_frag(yb + k * kTrChunk * kTrTile, 64 * wo + 16 * m, lane);
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+      for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(xb + k * kTrChunk * kTrTile, 64 * wi + 16 * n, lane);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = wmma(af[m], bfr[n], acc[m][n]);
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = wmma(af[m], bfr[n], acc[m][n]);
+    }
   }
   // partial tile: (o0 + 64wo + 16m + 4g + r, i0 + 64wi + 16n + c)
   float* pw = part_w + part * O * I;
@@ -272,6 +299,163 @@ wgrad_tr_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, const
       for (int k = 0; k < 16; ++k) sum += bsum_s[k][tid];
       part_b[part * O + o0 + tid] = sum;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The same tile and MFMA schedule, staged by LDS-DMA (global_load_lds_dwordx4)
+// through a 4-slot ring: chunk k+3 is issued while chunk k is computed, so
+// three chunks (48 KB per workgroup) are in flight instead of one held in
+// registers.  rocprofv3 counters on the register-staged kernel (enc FFN
+// shape, 103 us): HBM bytes = the algorithmic 205 MB, LDS bank conflicts ~0,
+// waves waiting on memory 45 % of their cycles -- one chunk in flight per
+// workgroup does not cover the load latency.
+// A DMA wave-instruction writes 64 lanes x 16 B contiguously: rows
+// 8 wave + 4 j + lane / 16 of the [32][128] image, position lane % 16; the
+// XOR swizzle of tr_elem goes on the SOURCE column (chunk p ^ swz(r)).
+// Columns past O / I read column 0 of the tile instead (their products land
+// only in accumulator rows / columns the epilogue does not store).  Only
+// whole 32-token chunks go through the ring; a split's token tail is staged
+// through registers with zero fill after the ring has drained.
+// Sync: counted vmcnt + raw s_barrier (a __syncthreads() would wait vmcnt(0)
+// and drain the ring; cdna_hip_programming.md §5, "Pipelining across
+// barriers"); the DMA is gd_common.h's asm GD_LDS_DMA16, which hipcc does not
+// track, so nothing else waits on it either.
+constexpr int kGlStages = 4;
+constexpr int kGlImg = kTrChunk * kTrTile;  // elements of one operand image (8 KB)
+constexpr int kGlStage = 2 * kGlImg;        // dY image, then X image
+
+__device__ __forceinline__ int tr_swz(int r) { return 2 * (r & 3) + 8 * ((r >> 3) & 1); }
+
+template <bool BIAS>
+__global__ void __launch_bounds__(256)
+wgrad_glds_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, const uint16_t* __restrict__ x,
+                  int64_t ldx, int64_t bsx, int T_, int O, int I, int splits, int tokens_per_split,
+                  float* __restrict__ part_w, float* __restrict__ part_b, int gx, int gy, int xcd_remap) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[kGlStages * kGlStage];  // the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int wo = wave >> 1, wi = wave & 1;  // the wave's 64 x 64 quarter
+  const int h = blockIdx.x;
+  const int L = xcd_remap ? xcd_logical(h, int(gridDim.x)) : h;
+  const int tile_i = L % gx, tile_o = (L / gx) % gy, zz = L / (gx * gy);
+  const int i0 = tile_i * kTrTile, o0 = tile_o * kTrTile;
+  const int bz = zz / splits, split = zz - bz * splits;
+  dy += bz * bsy;
+  x += bz * bsx;
+  const int64_t part = int64_t(bz) * splits + split;
+  const int tb = split * tokens_per_split;
+  const int te = min(T_, tb + tokens_per_split);
+  const bool do_bias = BIAS && tile_i == 0;
+  const int nfull = te > tb ? (te - tb) / kTrChunk : 0;
+  const int tail = te > tb ? (te - tb) - nfull * kTrChunk : 0;
+
+  // this lane's DMA sources: rows ra = 8 wave + lane / 16 and ra + 4 (same swizzle)
+  const int ra = 8 * wave + (lane >> 4);
+  const int pc = 8 * ((lane & 15) ^ tr_swz(ra));
+  const int ycol = o0 + pc < O ? o0 + pc : o0;
+  const int xcol = i0 + pc < I ? i0 + pc : i0;
+  const uint16_t* ysrc = dy + int64_t(tb + ra) * ldy + ycol;
+  const uint16_t* xsrc = x + int64_t(tb + ra) * ldx + xcol;
+  uint16_t* const wdst = lds + 8 * wave * kTrTile;  // + slot * kGlStage (+ kGlImg for X)
+  auto issue = [&](int k) {
+    uint16_t* d = wdst + (k % kGlStages) * kGlStage;
+    const int64_t ry = int64_t(k) * kTrChunk * ldy, rx = int64_t(k) * kTrChunk * ldx;
+    GD_LDS_DMA16(ysrc + ry, d);
+    GD_LDS_DMA16(ysrc + ry + 4 * ldy, d + 4 * kTrTile);
+    GD_LDS_DMA16(xsrc + rx, d + kGlImg);
+    GD_LDS_DMA16(xsrc + rx + 4 * ldx, d + kGlImg + 4 * kTrTile);
+  };
+
+  gd_f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // waves wi == 0: column 64 wo + 16 m + c, tokens 8g..8g+7 of each chunk
+
+  auto compute = [&](int slot) {
+    const uint16_t* yb = lds + slot * kGlStage;
+    const uint16_t* xb = yb + kGlImg;
+    WFrag<uint16_t> af[4], bfr[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) af[m] = tr_frag(yb, 64 * wo + 16 * m, lane);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(xb, 64 * wi + 16 * n, lane);
+    if (do_bias && wi == 0) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[m] += float(af[m].v[j]);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = wmma(af[m], bfr[n], acc[m][n]);
+  };
+
+  for (int k = 0; k < 3 && k < nfull; ++k) issue(k);
+  for (int k = 0; k < nfull; ++k) {
+    const int ahead = min(nfull - 1 - k, 2);  // chunks issued after k, still allowed in flight
+    if (ahead == 2)
+      gd_wait_vmcnt(8);
+    else if (ahead == 1)
+      gd_wait_vmcnt(4);
+    else
+      gd_wait_vmcnt(0);
+    gd_raw_barrier();  // every wave's chunk-k DMA landed; every wave done with chunk k - 1
+    if (k + 3 < nfull) issue(k + 3);  // slot (k + 3) % 4 held chunk k - 1
+    compute(k % kGlStages);
+  }
+  if (tail > 0) {  // ring drained (vmcnt(0) at its last chunk); stage the tail through registers
+    gd_wait_vmcnt(0);
+    gd_raw_barrier();
+    const int slot = nfull % kGlStages;
+    uint16_t* yb = lds + slot * kGlStage;
+    uint16_t* xb = yb + kGlImg;
+    const int t0 = tb + nfull * kTrChunk;
+    const int lrow = tid >> 4, lch = tid & 15;
+    const bool yok = o0 + 8 * lch < O, xok = i0 + 8 * lch < I;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int t = t0 + lrow + 16 * hh;
+      const bool in = t < te;
+      const uint4 vy = (in && yok) ? *reinterpret_cast<const uint4*>(dy + int64_t(t) * ldy + o0 + 8 * lch)
+                                   : make_uint4(0u, 0u, 0u, 0u);
+      const uint4 vx = (in && xok) ? *reinterpret_cast<const uint4*>(x + int64_t(t) * ldx + i0 + 8 * lch)
+                                   : make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(yb + tr_elem(lrow + 16 * hh, lch)) = vy;
+      *reinterpret_cast<uint4*>(xb + tr_elem(lrow + 16 * hh, lch)) = vx;
+    }
+    __syncthreads();
+    compute(slot);
+  }
+  // partial tile: (o0 + 64wo + 16m + 4g + r, i0 + 64wi + 16n + c)
+  float* pw = part_w + part * O * I;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = o0 + 64 * wo + 16 * m + 4 * g + r;
+      if (o < O) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int i = i0 + 64 * wi + 16 * n + c;
+          if (i < I) pw[int64_t(o) * I + i] = acc[m][n][r];
+        }
+      }
+    }
+  if (do_bias) {  // sum the 4 token groups of each column through LDS (ring no longer in use)
+    gd_wait_vmcnt(0);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [4 groups][128 columns]
+    if (wi == 0) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) red[g * kTrTile + 64 * wo + 16 * m + c] = bsum[m];
+    }
+    __syncthreads();
+    if (tid < kTrTile && o0 + tid < O)
+      part_b[part * O + o0 + tid] = red[tid] + red[kTrTile + tid] + red[2 * kTrTile + tid] + red[3 * kTrTile + tid];
   }
 }
 
@@ -334,6 +518,48 @@ wgrad_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ 
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// A/B knobs, read once: GD_WGRAD_GLDS=0 (the register-staged kernel instead
+// of the LDS-DMA ring), GD_WGRAD_CHUNK (its tokens per chunk, 32 | 64),
+// GD_WGRAD_XCD=0 (no XCD remap), GD_WGRAD_WGS (the workgroup count the split
+// choice aims for)
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+int tr_chunk() {
+  static const int v = env_int("GD_WGRAD_CHUNK", 32) == 64 ? 64 : 32;
+  return v;
+}
+int xcd_remap() {
+  static const int v = env_int("GD_WGRAD_XCD", 1) != 0;
+  return v;
+}
+int target_wgs() {  // 0: the per-shape default
+  static const int v = env_int("GD_WGRAD_WGS", 0) > 0 ? env_int("GD_WGRAD_WGS", 0) : 0;
+  return v;
+}
+
+int glds_on() {
+  static const int v = env_int("GD_WGRAD_GLDS", 1) != 0;
+  return v;
+}
+
+template <bool BIAS>
+void launch_tr(int gx, int gy, int gz, hipStream_t s, const uint16_t* dy, int64_t ldy, int64_t bsy, const uint16_t* x,
+               int64_t ldx, int64_t bsx, int T, int O, int I, int splits, int tps, float* pw, float* pb) {
+  const dim3 grid(unsigned(gx * gy * gz));
+  const int remap = xcd_remap();
+  if (glds_on())
+    hipLaunchKernelGGL((wgrad_glds_kernel<BIAS>), grid, dim3(256), 0, s, dy, ldy, bsy, x, ldx, bsx, T, O, I, splits,
+                       tps, pw, pb, gx, gy, remap);
+  else if (tr_chunk() == 64)
+    hipLaunchKernelGGL((wgrad_tr_kernel<BIAS, 64>), grid, dim3(256), 0, s, dy, ldy, bsy, x, ldx, bsx, T, O, I, splits,
+                       tps, pw, pb, gx, gy, remap);
+  else
+    hipLaunchKernelGGL((wgrad_tr_kernel<BIAS, 32>), grid, dim3(256), 0, s, dy, ldy, bsy, x, ldx, bsx, T, O, I, splits,
+                       tps, pw, pb, gx, gy, remap);
+}
+
 }  // namespace
 }  // namespace gd
 
@@ -348,7 +574,12 @@ extern "C" int gd_wgrad_splits_batched(int T, int O, int I, int batch) {
   // 128 tokens each: the fp32 partials (splits x O x I) stay a fraction of
   // the token-major inputs the kernel streams
   const int tiles = ((O + kTrTile - 1) / kTrTile) * ((I + kTrTile - 1) / kTrTile) * (batch > 0 ? batch : 1);
-  int s = tiles > 0 ? (384 + tiles - 1) / tiles : 1;
+  // 384 workgroups; 512 when a split has 16+ output tiles (FFN-sized weights,
+  // the batched BiAttention products): there the extra splits' partials cost
+  // less than the added loads in flight win (tools/wgrad_microbench.py,
+  // profiles/r04c_wgrad_ab.jsonl: enc FFN 88 -> 75 us, 256 x 256 worse)
+  const int wgs = target_wgs() > 0 ? target_wgs() : (tiles >= 16 ? 512 : 384);
+  int s = tiles > 0 ? (wgs + tiles - 1) / tiles : 1;
   const int cap = T / 128 > 1 ? T / 128 : 1;
   return s < 1 ? 1 : (s > cap ? cap : s);
 }
@@ -379,19 +610,19 @@ extern "C" gd_status gd_wgrad_batched(gd_dtype dt, const void* grad_y, int64_t l
   hipStream_t s = as_hip(stream);
   float* part_w = static_cast<float*>(workspace);
   float* part_b = part_w + int64_t(batch) * splits * O * I;
-  const int tps = ((T + splits - 1) / splits + kWgChunk - 1) / kWgChunk * kWgChunk;
   if (dt == GD_BF16) {
-    const dim3 grid(unsigned((I + kTrTile - 1) / kTrTile), unsigned((O + kTrTile - 1) / kTrTile),
-                    unsigned(batch * splits));
+    const int ch = tr_chunk();
+    const int tps = ((T + splits - 1) / splits + ch - 1) / ch * ch;
+    const int gx = (I + kTrTile - 1) / kTrTile, gy = (O + kTrTile - 1) / kTrTile;
+    GD_REQUIRE(int64_t(gx) * gy * batch * splits < (int64_t(1) << 31), "wgrad: grid too large");
     if (grad_b)
-      hipLaunchKernelGGL((wgrad_tr_kernel<true>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy,
-                         batch_stride_y, (const uint16_t*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
-                         part_b);
+      launch_tr<true>(gx, gy, batch * splits, s, (const uint16_t*)grad_y, ldy, batch_stride_y, (const uint16_t*)x,
+                      ldx, batch_stride_x, T, O, I, splits, tps, part_w, part_b);
     else
-      hipLaunchKernelGGL((wgrad_tr_kernel<false>), grid, dim3(256), 0, s, (const uint16_t*)grad_y, ldy,
-                         batch_stride_y, (const uint16_t*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,
-                         nullptr);
+      launch_tr<false>(gx, gy, batch * splits, s, (const uint16_t*)grad_y, ldy, batch_stride_y, (const uint16_t*)x,
+                       ldx, batch_stride_x, T, O, I, splits, tps, part_w, nullptr);
   } else {
+    const int tps = ((T + splits - 1) / splits + kWgChunk - 1) / kWgChunk * kWgChunk;
     const dim3 grid(unsigned(I / 64), unsigned(O / 64), unsigned(batch * splits));
     hipLaunchKernelGGL((wgrad_kernel<float>), grid, dim3(256), 0, s, (const float*)grad_y, ldy, batch_stride_y,
                        (const float*)x, ldx, batch_stride_x, T, O, I, splits, tps, part_w,

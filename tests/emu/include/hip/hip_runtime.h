@@ -346,6 +346,18 @@ inline C4 mfma_16x16x4_f32(float a, float b, C4 c) {
 
 void syncthreads();
 
+// global_load_lds_dwordx4 (gd_common.h GD_LDS_DMA16): the LDS destination is
+// the wave-uniform base (M0, from the first lane) + 16 * lane; the source is
+// per lane.  The emulator's memory is synchronous, so the data lands at once
+// (an early ds_read of a slot still shows what the kernel's ordering allows:
+// the poisoned or previous contents until a barrier-ordered DMA wrote it).
+inline void lds_dma16(const void* src, void* dst) {
+  const uint64_t mine = uint64_t(uintptr_t(dst));
+  uint64_t all[64];
+  wave_gather(&mine, sizeof(mine), all);
+  memcpy(reinterpret_cast<char*>(uintptr_t(all[0])) + 16 * lane_id(), src, 16);
+}
+
 template <typename F>
 void launch(dim3 g, dim3 b, F&& f) {
   auto thunk = [](void* p) { (*static_cast<F*>(p))(); };
@@ -367,6 +379,9 @@ inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 #define __shfl_xor(v, mask, width) ::gd_emu::shfl_xor((v), (mask), (width))
 #define __shfl(v, src, width) ::gd_emu::shfl((v), (src), (width))
 #define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
+#define __builtin_amdgcn_s_barrier() ::gd_emu::syncthreads()
+#define __builtin_amdgcn_s_waitcnt(imm) ((void)(imm))  // memory is synchronous here
+#define GD_LDS_DMA16(src, dst) ::gd_emu::lds_dma16((const void*)(src), (void*)(dst))
 // compiler scheduling hints: no semantics to emulate
 #define __builtin_amdgcn_sched_barrier(mask) ((void)(mask))
 #define __builtin_amdgcn_ds_read_tr16_b64_v4i16(p) ::gd_emu::ds_read_tr16_b64((const void*)(uintptr_t)(p))

@@ -18,6 +18,8 @@ def emulated_product(min_tokens=None):
     from gdino_amd import _lib, wgrad
     emu = emu_lib.lib()
     for name, argtypes in _lib._SIGNATURES.items():
+        if name.startswith("gd_graph_"):  # HIP graph editing: runtime API, not a kernel (no emulator twin)
+            continue
         fn = getattr(emu, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int

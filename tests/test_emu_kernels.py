@@ -780,6 +780,7 @@ def test_emulated_msda_prologue(ref_dim, dtype):
     (333, 48, 80, 2, torch.bfloat16, 1e-6),       # bf16 128-tile kernel: O, I multiples of 16, partial tiles
     (700, 384, 256, 3, torch.bfloat16, 1e-6),     # bf16: 3 x 2 tiles, token tail
     (96, 16, 16, 7, torch.bfloat16, 1e-6),        # bf16: empty splits, one 16-wide column
+    (2000, 128, 144, 2, torch.bfloat16, 1e-6),    # bf16: 31 whole chunks per split through the 4-slot DMA ring
 ])
 def test_emulated_wgrad(T, O, I, splits, dtype, tol):
     g = torch.Generator().manual_seed(T + O)

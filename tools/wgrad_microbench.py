@@ -41,6 +41,7 @@ def time_it(fn, iters=20, warm=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-lib", action="store_true", help="skip the library GEMM timings")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
     for name, t, o, i in SHAPES:
@@ -48,13 +49,17 @@ def main():
         x = torch.randn(t, i, generator=g, device="cuda").to(torch.bfloat16)
         flops = 2.0 * t * o * i
         mine = time_it(lambda: wgrad.weight_grad(dy, x, True), a.iters)
-        lib = time_it(lambda: wgrad.weight_grad_lib(dy, x, True), a.iters)  # bf16 x bf16 -> fp32 GEMM + fp32 sum
+        lib = (float("nan") if a.no_lib else  # bf16 x bf16 -> fp32 GEMM + fp32 sum
+               time_it(lambda: wgrad.weight_grad_lib(dy, x, True), a.iters))
         dw, db = wgrad.weight_grad(dy, x, True)
         ref = dy.double().t() @ x.double()
         err = float((dw.double() - ref).abs().max() / ref.abs().max())
         berr = float((db.double() - dy.double().sum(0)).abs().max() / dy.double().sum(0).abs().max())
-        print(json.dumps(dict(shape=name, T=t, O=o, I=i, splits=wgrad._splits(t, o, i), mine_us=mine * 1e6,
-                              lib_us=lib * 1e6, mine_tflops=flops / mine / 1e12, lib_tflops=flops / lib / 1e12,
+        nbytes = 2.0 * t * (o + i) + 4.0 * o * (i + 1)  # bf16 dY and X once, fp32 dW and db
+        print(json.dumps(dict(variant=os.environ.get("GD_WGRAD_CHUNK", "32") + "/" +
+                              os.environ.get("GD_WGRAD_WGS", "384"),
+                              shape=name, T=t, O=o, I=i, splits=wgrad._splits(t, o, i), mine_us=mine * 1e6,
+                              mine_tbs=nbytes / mine / 1e12, lib_us=lib * 1e6, mine_tflops=flops / mine / 1e12, lib_tflops=flops / lib / 1e12,
                               mfma_frac=flops / mine / PEAK, rel_err_w=err, rel_err_b=berr)), flush=True)
     # BiAttention's batched long-K products (biattn.py: 8 (b, h) x 22 223 tokens x 256 x 256)
     a_ = torch.randn(8, 22223, 256, generator=g, device="cuda").to(torch.bfloat16)
