@@ -430,23 +430,36 @@ wgrad_glds_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, con
     __syncthreads();
     compute(slot);
   }
-  // partial tile: (o0 + 64wo + 16m + 4g + r, i0 + 64wi + 16n + c)
+  // partial tile (o0 + 64wo + 16m + 4g + r, i0 + 64wi + 16n + c), through LDS
+  // in two 64-row halves so that it leaves as 16-B row stores (512 B per
+  // row) rather than 4-B stores in 64-B pieces: a 128 x 128 partial is 64 KB
+  // per workgroup, written by every split.  Pitch 132 floats: the 16 lanes
+  // c and 4 groups g of one ds_write hit 64 distinct banks.
+  constexpr int kEpPitch = kTrTile + 4;
+  float* ep = reinterpret_cast<float*>(lds);
   float* pw = part_w + part * O * I;
+  gd_wait_vmcnt(0);
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();  // the ring's last reads / the previous half's row reads are done
+    if (wo == half) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = o0 + 64 * wo + 16 * m + 4 * g + r;
-      if (o < O) {
+      for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int i = i0 + 64 * wi + 16 * n + c;
-          if (i < I) pw[int64_t(o) * I + i] = acc[m][n][r];
-        }
-      }
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) ep[(16 * m + 4 * g + r) * kEpPitch + 64 * wi + 16 * n + c] = acc[m][n][r];
     }
+    __syncthreads();
+#pragma unroll
+    for (int v = tid; v < 64 * (kTrTile / 4); v += 256) {
+      const int rr = v / (kTrTile / 4), q = v % (kTrTile / 4);
+      const int o = o0 + 64 * half + rr, i = i0 + 4 * q;
+      if (o < O && i < I)
+        *reinterpret_cast<float4*>(pw + int64_t(o) * I + i) = *reinterpret_cast<const float4*>(ep + rr * kEpPitch + 4 * q);
+    }
+  }
   if (do_bias) {  // sum the 4 token groups of each column through LDS (ring no longer in use)
-    gd_wait_vmcnt(0);
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);  // [4 groups][128 columns]
     if (wi == 0) {
