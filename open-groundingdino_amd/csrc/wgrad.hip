@@ -451,7 +451,6 @@ wgrad_glds_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, con
           for (int n = 0; n < 4; ++n) ep[(16 * m + 4 * g + r) * kEpPitch + 64 * wi + 16 * n + c] = acc[m][n][r];
     }
     __syncthreads();
-#pragma unroll
     for (int v = tid; v < 64 * (kTrTile / 4); v += 256) {
       const int rr = v / (kTrTile / 4), q = v % (kTrTile / 4);
       const int o = o0 + 64 * half + rr, i = i0 + 4 * q;

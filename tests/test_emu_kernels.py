@@ -438,7 +438,18 @@ t.test_emulated_add_layernorm(41, 96, torch.float32, None)
 t._check_bwd(t._levels_inputs(t.WIDE, 1, sum(h * w for h, w in t.WIDE), seed=4, local=True, outlier_frac=0.02), 1e-5)
 t.test_emulated_biattn_softmax(torch.bfloat16, 1e-2, (1, 2, 200, 100))
 t.test_emulated_biattn_softmax(torch.float32, 1e-5, (2, 1, 260, 128))
-t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5)
+import os
+
+
+class _Env:  # the monkeypatch argument of the contrastive test
+    @staticmethod
+    def setenv(k, v):
+        os.environ[k] = v
+
+
+for wide in ("0", "1"):
+    t.test_emulated_contrastive(2, 100, 37, 64, 256, torch.float32, 1e-5, wide, _Env)
+os.environ.pop("GD_CONTRASTIVE_WIDE", None)
 t.test_emulated_msda_prologue(2, torch.bfloat16)
 t.test_emulated_msda_prologue(4, torch.float32)
 t.test_emulated_window_attention_image(1, 9, 11, 7, 3, 3, True, torch.bfloat16, 1.5e-2, True)
@@ -446,6 +457,8 @@ t.test_emulated_window_attention_image(1, 14, 17, 12, 6, 1, True, torch.bfloat16
 """,
     r"""
 t.test_emulated_window_attention(7, 2, 22, 1, False, torch.float32, 1e-5, True)
+t.test_emulated_wgrad(2000, 128, 144, 2, torch.bfloat16, 1e-6)  # the LDS-DMA ring, column clamp, token tail
+t.test_emulated_wgrad(333, 48, 80, 2, torch.bfloat16, 1e-6)
 t.test_emulated_window_attention(3, 4, 6, 3, True, torch.bfloat16, 1.5e-2, False)
 t.test_emulated_window_attention(12, 2, 4, 2, True, torch.float32, 1e-5, True)
 t.test_emulated_attention(2, 2, 130, 40, 32, "keypad", torch.float32, 1e-5, "lbh")
