@@ -372,7 +372,16 @@ wgrad_glds_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, con
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = zero4();
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // waves wi == 0: column 64 wo + 16 m + c, tokens 8g..8g+7 of each chunk
+  // db on the matrix cores: waves wi == 0 multiply their dY^T fragments by an
+  // all-ones B operand (4 MFMAs per chunk instead of 64 VALU conversions and
+  // adds, which made the bias workgroups the stragglers); every column of
+  // accb[m] holds the row sums of rows 64 wo + 16 m + 4 g + r
+  gd_f32x4 accb[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) accb[m] = zero4();
+  WFrag<uint16_t> ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones.v[j] = __builtin_bit_cast(__bf16, uint16_t(0x3F80));
 
   auto compute = [&](int slot) {
     const uint16_t* yb = lds + slot * kGlStage;
@@ -384,9 +393,7 @@ wgrad_glds_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, con
     for (int n = 0; n < 4; ++n) bfr[n] = tr_frag(xb, 64 * wi + 16 * n, lane);
     if (do_bias && wi == 0) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bsum[m] += float(af[m].v[j]);
+      for (int m = 0; m < 4; ++m) accb[m] = wmma(af[m], ones, accb[m]);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -458,16 +465,14 @@ wgrad_glds_kernel(const uint16_t* __restrict__ dy, int64_t ldy, int64_t bsy, con
         *reinterpret_cast<float4*>(pw + int64_t(o) * I + i) = *reinterpret_cast<const float4*>(ep + rr * kEpPitch + 4 * q);
     }
   }
-  if (do_bias) {  // sum the 4 token groups of each column through LDS (ring no longer in use)
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(lds);  // [4 groups][128 columns]
-    if (wi == 0) {
+  if (do_bias && wi == 0 && c == 0) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) red[g * kTrTile + 64 * wo + 16 * m + c] = bsum[m];
-    }
-    __syncthreads();
-    if (tid < kTrTile && o0 + tid < O)
-      part_b[part * O + o0 + tid] = red[tid] + red[kTrTile + tid] + red[2 * kTrTile + tid] + red[3 * kTrTile + tid];
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + 64 * wo + 16 * m + 4 * g + r;
+        if (o < O) part_b[part * O + o] = accb[m][r];
+      }
   }
 }
 
