@@ -445,18 +445,25 @@ def test_msda_prologue_matches_composition(dtype, ref_dim, lq):
 
 
 # ----------------------------------------- split-K weight gradient (HIP)
-@pytest.mark.parametrize("T,O,I", [(44446, 256, 256), (44446, 384, 256), (33400, 192, 192), (5000, 128, 64)])
+@pytest.mark.parametrize("T,O,I", [(44446, 256, 256), (44446, 384, 256), (33400, 192, 192), (5000, 128, 64),
+                                   (44446, 2048, 256),   # FFN: 16+ tiles per split (512-workgroup target)
+                                   (2001, 48, 80),       # partial tiles (source-column clamp), token tail
+                                   (66800, 96, 96)])     # Swin stage 0 width, I < one 128 tile
 def test_wgrad_kernel(T, O, I):
     """encoder value / output / sampling projections at 800x1333 bs=2, Swin
-    stage-2 width; bf16 operands, fp32 results vs the fp64 product."""
+    stage widths, the FFN; bf16 operands, fp32 results vs the fp64 product
+    (the LDS-DMA ring kernel, db by MFMA against ones); dW without the bias
+    is bitwise the same."""
     from gdino_amd.wgrad import weight_grad
     g = torch.Generator().manual_seed(T + O)
     dy = torch.randn(T, O, generator=g).to(torch.bfloat16)
     x = torch.randn(T, I, generator=g).to(torch.bfloat16)
     dw, db = weight_grad(dy.to(DEV), x.to(DEV), True)
+    dw2, none = weight_grad(dy.to(DEV), x.to(DEV), False)
     torch.cuda.synchronize()
     assert _rel(dw.cpu(), dy.double().t() @ x.double()) < 1e-5
     assert _rel(db.cpu(), dy.double().sum(0)) < 1e-5
+    assert none is None and torch.equal(dw, dw2)
 
 
 def test_token_linear_matches_autocast_linear():
