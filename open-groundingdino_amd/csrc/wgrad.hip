@@ -506,13 +506,27 @@ wgrad_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ 
     stride = nb4;
   }
   if (src) {
-    for (int k = grp; k < splits; k += kRedGroups) {
-      const float4 v = src[int64_t(k) * stride];
+    // four independent loads in flight per step (hipcc otherwise issued one
+    // load and waited for it per split: 12 serial round trips at 96 splits);
+    // the adds keep the split order, so the sums are unchanged bit for bit
+    auto acc4 = [&](float4 v) {
       s.x += v.x;
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
+    };
+    int k = grp;
+    for (; k + 3 * kRedGroups < splits; k += 4 * kRedGroups) {
+      const float4 v0 = src[int64_t(k) * stride];
+      const float4 v1 = src[int64_t(k + kRedGroups) * stride];
+      const float4 v2 = src[int64_t(k + 2 * kRedGroups) * stride];
+      const float4 v3 = src[int64_t(k + 3 * kRedGroups) * stride];
+      acc4(v0);
+      acc4(v1);
+      acc4(v2);
+      acc4(v3);
     }
+    for (; k < splits; k += kRedGroups) acc4(src[int64_t(k) * stride]);
   }
   red[grp][col] = s;
   __syncthreads();
