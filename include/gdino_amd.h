@@ -426,6 +426,29 @@ gd_status gd_add_scaled_backward(gd_dtype g_dtype, const void* grad_out, gd_dtyp
                                  void* workspace, gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* Box refinement: out = sigmoid(delta + inverse_sigmoid(ref))               */
+/* ------------------------------------------------------------------------ */
+/*
+ * Replaces the composition `delta + inverse_sigmoid(ref)` then `.sigmoid()`
+ * of the decoder's anchor update (reference transformer.py:728-731) and the
+ * per-layer box heads (reference groundingdino.py:325-327), inverse_sigmoid
+ * as reference util/misc.py:614-618 (clamp to [0, 1], then log(max(x, eps) /
+ * max(1 - x, eps))).  Python: gdino_amd.misc.box_refine.
+ *
+ * delta [n0, n1, n2] fp32 / bf16 and ref fp32, each with its own element
+ * strides (ds*, rs*); out fp32 contiguous [n0, n1, n2].  Backward: grad_out
+ * and out (the forward's result) contiguous fp32; grad_delta (delta's dtype)
+ * and grad_ref (fp32) contiguous, either may be NULL.  The gradients are
+ * autograd's for the composition (clamp masks inclusive; NaN ref -> 0).
+ */
+gd_status gd_box_refine_forward(gd_dtype delta_dtype, const void* delta, int64_t ds0, int64_t ds1, int64_t ds2,
+                                const float* ref, int64_t rs0, int64_t rs1, int64_t rs2, int64_t n0, int64_t n1,
+                                int64_t n2, float eps, float* out, gd_stream_t stream);
+gd_status gd_box_refine_backward(gd_dtype delta_dtype, const float* grad_out, const float* out, const float* ref,
+                                 int64_t rs0, int64_t rs1, int64_t rs2, int64_t n0, int64_t n1, int64_t n2,
+                                 float eps, void* grad_delta, float* grad_ref, gd_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Captured-graph surgery (the train step as one HIP graph)                  */
 /* ------------------------------------------------------------------------ */
 /*

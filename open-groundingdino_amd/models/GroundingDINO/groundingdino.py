@@ -36,7 +36,8 @@ from torch import nn
 
 from gdino_amd import box_ops, castcache
 from gdino_amd.conv import GemmConv2d
-from gdino_amd.misc import (NestedTensor, no_padding, get_world_size, inverse_sigmoid, is_dist_avail_and_initialized,
+from gdino_amd.misc import (NestedTensor, box_refine, no_padding, get_world_size,
+                            is_dist_avail_and_initialized,
                             nested_tensor_from_tensor_list)
 from gdino_amd.tokenizer import get_pretrained_language_model, get_tokenlizer
 
@@ -240,7 +241,7 @@ class GroundingDINO(nn.Module):
 
         coords = []
         for ref_sig, box_embed, layer_hs in zip(reference[:-1], self.bbox_embed, hs):
-            coords.append((box_embed(layer_hs) + inverse_sigmoid(ref_sig)).sigmoid())
+            coords.append(box_refine(box_embed(layer_hs), ref_sig))  # groundingdino.py:325-327
         outputs_coord = torch.stack(coords)
         outputs_class = torch.stack([emb(layer_hs, text_dict) for emb, layer_hs in zip(self.class_embed, hs)])
         bs, len_td = text_dict["text_token_mask"].shape

@@ -25,7 +25,7 @@ from torch import Tensor, nn
 from gdino_amd import kernels
 from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
-from gdino_amd.misc import device_const, inverse_sigmoid, no_padding, padding_free, topk_indices
+from gdino_amd.misc import box_refine, device_const, no_padding, padding_free, topk_indices
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
@@ -338,7 +338,7 @@ class TransformerDecoder(nn.Module):
                 print(f"output layer_id {layer_id} is nan: num_nan {int(output.isnan().sum())}, "
                       f"num_inf {int(output.isinf().sum())}")
             if self.bbox_embed is not None:
-                new_ref = (self.bbox_embed[layer_id](output) + inverse_sigmoid(reference_points)).sigmoid()
+                new_ref = box_refine(self.bbox_embed[layer_id](output), reference_points)  # transformer.py:728-731
                 reference_points = new_ref.detach()
                 ref_points.append(new_ref)
             intermediate.append(self.norm(output))

@@ -842,6 +842,55 @@ def test_emulated_add_layernorm(rows, C, xd, rd):
     assert E.rel_err(db, bd.grad) < 1e-5
 
 
+# ------------------------------------------------ box refinement (boxref.hip)
+@pytest.mark.parametrize("dd,transposed_ref,ref_grad", [
+    (torch.float32, False, True),
+    (torch.bfloat16, True, True),    # the box heads: bf16 MLP output, reference points through a transposed view
+    (torch.bfloat16, False, False),  # the decoder's anchor update: detached reference points
+])
+def test_emulated_box_refine(dd, transposed_ref, ref_grad, monkeypatch):
+    """sigmoid(delta + inverse_sigmoid(ref)) forward / backward through the
+    product's autograd function vs the composition (GDINO_DISABLE=boxrefine),
+    including reference points outside [0, 1], at the clamp edges (0, 1,
+    eps, 1 - eps) and NaN."""
+    from emu_product import emulated_product
+    from gdino_amd.misc import box_refine
+    g = torch.Generator().manual_seed(7)
+    delta = torch.randn(2, 37, 4, generator=g).to(dd)
+    ref = torch.rand(37, 2, 4, generator=g) * 1.2 - 0.1
+    ref.view(-1)[:8] = torch.tensor([0.0, 1.0, 1e-3, 1 - 1e-3, 5e-4, 0.9996, -0.0, float("nan")])
+    ref = ref.transpose(0, 1) if transposed_ref else ref.transpose(0, 1).contiguous()
+    go = torch.randn(2, 37, 4, generator=g)
+
+    def run(disable):
+        if disable:
+            monkeypatch.setenv("GDINO_DISABLE", "boxrefine")
+        else:
+            monkeypatch.delenv("GDINO_DISABLE", raising=False)
+        d = delta.clone().requires_grad_(True)
+        r = ref.detach().clone() if not transposed_ref else ref.detach().transpose(0, 1).clone().transpose(0, 1)
+        r.requires_grad_(ref_grad)
+        with emulated_product():
+            out = box_refine(d, r)
+            out.backward(go)
+        return out.detach(), d.grad, r.grad
+
+    got, want = run(False), run(True)
+    assert got[0].dtype == want[0].dtype == torch.float32
+    assert torch.equal(got[0].isnan(), want[0].isnan())
+    fin = ~want[0].isnan()
+    assert E.rel_err(got[0][fin], want[0][fin]) < 1e-6
+    assert got[1].dtype == dd
+    gfin = ~want[1].float().isnan()
+    assert E.rel_err(got[1].float()[gfin], want[1].float()[gfin]) < (1e-6 if dd == torch.float32 else 2 ** -7)
+    if ref_grad:
+        assert torch.equal(got[2].isnan(), want[2].isnan())
+        rf = ~want[2].isnan()
+        assert E.rel_err(got[2][rf], want[2][rf]) < 1e-5
+    else:
+        assert got[2] is None and want[2] is None
+
+
 @pytest.mark.parametrize("n,c,bd,sshape,sd,xd", [
     (37, 96, torch.bfloat16, (2, 1, 96), torch.float32, torch.float32),    # layer scale x drop path
     (300, 256, torch.bfloat16, (2, 1, 1), torch.bfloat16, torch.float32),  # drop path only, bf16 mask

@@ -718,3 +718,32 @@ def test_add_scaled_matches_composition(shape, bd, sshape, sd, monkeypatch):
         tol = {"out": 1e-6 if a.dtype == torch.float32 else 2 ** -7, "dx": 0.0,
                "dbranch": 2 ** -7, "ds": 1e-4 if sd == torch.float32 else 1e-2}[name]
         assert _rel(a, b) <= tol, (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("dd", [torch.float32, torch.bfloat16])
+def test_box_refine_matches_composition(dd, monkeypatch):
+    """csrc/boxref.hip: sigmoid(delta + inverse_sigmoid(ref)) forward and
+    backward on the device vs the composition (GDINO_DISABLE=boxrefine) at
+    the decoder's shape, reference points through a transposed view."""
+    from gdino_amd.misc import box_refine
+    g = torch.Generator().manual_seed(3)
+    delta = torch.randn(2, 900, 4, generator=g).to(dd).to(DEV)
+    ref = (torch.rand(900, 2, 4, generator=g) * 1.2 - 0.1).to(DEV)
+    go = torch.randn(2, 900, 4, generator=g).to(DEV)
+
+    def run(disable):
+        if disable:
+            monkeypatch.setenv("GDINO_DISABLE", "boxrefine")
+        else:
+            monkeypatch.delenv("GDINO_DISABLE", raising=False)
+        d = delta.clone().requires_grad_(True)
+        r = ref.clone().requires_grad_(True)
+        out = box_refine(d, r.transpose(0, 1))
+        out.backward(go)
+        torch.cuda.synchronize()
+        return out.detach().cpu(), d.grad.float().cpu(), r.grad.cpu()
+
+    got, want = run(False), run(True)
+    assert _rel(got[0], want[0]) < 1e-6
+    assert _rel(got[1], want[1]) < (1e-6 if dd == torch.float32 else 2 ** -7)
+    assert _rel(got[2], want[2]) < 1e-5

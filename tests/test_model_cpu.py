@@ -409,9 +409,12 @@ def test_padding_free_batch_skips_only_an_identity_mask():
     assert torch.equal(res[True][0], res[False][0])
     for n, g in res[True][1].items():
         # (the autograd engine may sum a tensor's incoming gradients in
-        # another order without the masked_fill node: fp32 rounding apart)
+        # another order without the masked_fill node, and the CPU's threaded
+        # reductions -- e.g. a relative-position-bias table summed over every
+        # window -- need not repeat their order: fp32 rounding apart, seen up
+        # to 1.1e-6 of the tensor's max)
         r = res[False][1][n]
-        assert float((g - r).abs().max()) <= 1e-6 * float(r.abs().max().clamp_min(1e-30)), n
+        assert float((g - r).abs().max()) <= 1e-5 * float(r.abs().max().clamp_min(1e-30)), n
     a, b = torch.zeros(3, 8, 8), torch.zeros(3, 6, 8)
     assert nested_tensor_from_tensor_list([a, a]).padding_free
     assert not nested_tensor_from_tensor_list([a, b]).padding_free
