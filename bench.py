@@ -71,6 +71,12 @@ def parse(argv=None):
     ap.add_argument("--output-dir", default=None,
                     help="reference main.py:347-434: resume from DIR/checkpoint.pth when present, save it after "
                          "the timed steps (rank 0); outside the timed region")
+    ap.add_argument("--ckpt-compare", choices=("auto", "on", "off"), default="auto",
+                    help="also time the reference configuration (activation checkpointing on) in the same run and "
+                         "report it under config.value_ckpt_on (auto: with HIP graphs)")
+    ap.add_argument("--timeout", type=float, default=600.0,
+                    help="bound (s) on every device wait and host barrier: a stuck collective or kernel ends the "
+                         "run with an error line instead of a hang")
     ap.add_argument("--device", choices=("cuda", "cpu"), default=None,
                     help=argparse.SUPPRESS)  # cpu: the CPU contract tests only (HIP ops routed by the test)
     return ap.parse_args(argv)
@@ -283,6 +289,85 @@ def _progress(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+METRIC = "train images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU"
+
+
+class BenchError(RuntimeError):
+    pass
+
+
+def _bounded_sync(on_gpu, timeout_s, what):
+    """torch.cuda.synchronize() with a deadline: a replay stuck in a
+    collective (or a hung kernel) becomes an error line instead of a silent
+    hang."""
+    if not on_gpu:
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    deadline = time.monotonic() + timeout_s
+    while not ev.query():
+        if time.monotonic() > deadline:
+            raise BenchError(f"device did not finish within {timeout_s:.0f} s: {what}")
+        time.sleep(2e-4)
+    torch.cuda.synchronize()
+
+
+def _barrier(world, ctrl):
+    """host barrier over the gloo control group (its timeout bounds it)"""
+    if world > 1:
+        dist.barrier(group=ctrl)
+
+
+def _max_over_ranks(x, world, ctrl):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl)
+    return float(t)
+
+
+def _timed(step, a, on_gpu, world, ctrl, what):
+    """W warm-up steps, then K timed steps bracketed by a barrier and a device
+    synchronisation on both sides; per-step device boundaries from one event
+    per step (no host sync inside the loop); the max elapsed over ranks."""
+    for _ in range(a.warmup):
+        step()
+    _bounded_sync(on_gpu, a.timeout, f"{what}: warm-up steps")
+    _barrier(world, ctrl)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if on_gpu else None
+    host_marks = []
+    loss = None
+    t0 = time.perf_counter()
+    if evs:
+        evs[0].record()
+    for i in range(a.steps):
+        loss = step()
+        if evs:
+            evs[i + 1].record()
+        host_marks.append(time.perf_counter())
+    _bounded_sync(on_gpu, a.timeout, f"{what}: timed steps")
+    _barrier(world, ctrl)
+    elapsed = time.perf_counter() - t0
+    if evs:
+        step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)]
+    else:
+        step_ms = [(b - a_) * 1e3 for a_, b in zip([t0] + host_marks[:-1], host_marks)]
+    return _max_over_ranks(elapsed, world, ctrl), _dist_stats(step_ms), float(loss)
+
+
+def _roofline(kern, bs, timed_note):
+    """dominant MSDA launch of a per-launch timing summary -> roofline dict"""
+    if not kern:
+        return None
+    kname, kd = max(kern.items(), key=lambda kv: kv[1]["ms"])
+    avg_s = kd["ms"] / kd["n"] * 1e-3
+    achieved = kd["bytes"] / avg_s
+    return {"bound": "hbm", "kernel": f"msda_{kname[0]} (Lq={kname[1]})",
+            "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": pmc_traffic(kname, bs),
+            "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"], "timed": timed_note}
+
+
 def main(argv=None, device_type="cuda", child_script=None):
     """device_type="cpu" exists for tests/test_bench_contract.py only (the
     HIP ops are then routed to the oracle by the test); the bench itself
@@ -302,8 +387,29 @@ def main(argv=None, device_type="cuda", child_script=None):
     on_gpu = device_type == "cuda"
     rank, world, local = setup_dist(a.gpus, on_gpu,
                                     capture=(a.graphs is not False) and on_gpu and not a.forward_only)
+    ctrl = None
+    if world > 1:
+        from gdino_amd.stepgraph import make_control_group
+        ctrl = make_control_group(a.timeout)
+    try:
+        _run(a, on_gpu, rank, world, local, ctrl)
+    except BenchError as e:
+        _error_line(a, world, rank, str(e))
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3)  # a rank stuck in a collective cannot be joined: leave now
+
+
+def _error_line(a, world, rank, msg):
+    print(f"bench error on rank {rank}: {msg}", file=sys.stderr, flush=True)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "images/s", "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "bf16", "error": msg}), flush=True)
+
+
+def _run(a, on_gpu, rank, world, local, ctrl):
     device = torch.device("cuda", local) if on_gpu else torch.device("cpu")
-    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     if on_gpu:
         torch.cuda.set_device(device)
     if a.tunableop:
@@ -312,12 +418,12 @@ def main(argv=None, device_type="cuda", child_script=None):
 
     from gdino_amd import _lib, msda
     from gdino_amd.config import make_args
-    from gdino_amd.train import build_training, forward_step, synthetic_batch, train_step
+    from gdino_amd.train import build_training, forward_step, set_activation_checkpointing, synthetic_batch, \
+        train_step
 
     args = make_args(device=str(device), backbone=a.backbone)
     model, criterion, _, optimizer = build_training(args, device)
     model.train(not a.forward_only)
-    from gdino_amd.train import set_activation_checkpointing
     set_activation_checkpointing(model, a.checkpointing == "on")
     _progress("model built")
     start_epoch = 0
@@ -339,7 +445,7 @@ def main(argv=None, device_type="cuda", child_script=None):
             # the same bucketed, backward-overlapped all-reduce from
             # post-accumulate hooks, captured into the step graph
             from gdino_amd.train import BucketedGradSync
-            grad_sync = BucketedGradSync(model.parameters(), a.bucket_mb)
+            grad_sync = BucketedGradSync(model.parameters(), a.bucket_mb, control_group=ctrl)
         else:
             # reference main.py:258-261 (DDP + static graph); buckets sized for
             # xGMI rings (fewer, larger all-reduces), launched as backward
@@ -356,75 +462,36 @@ def main(argv=None, device_type="cuda", child_script=None):
         def step():
             return train_step(model, criterion, optimizer, samples, targets, captions, cats, grad_sync=grad_sync)
 
-    graph_note = None
     eager_step = step
     step_graph = None
+
+    def make_graph_step():
+        from gdino_amd.stepgraph import TrainStepGraph
+        g = TrainStepGraph(core, criterion, optimizer, grad_sync=grad_sync, control_group=ctrl)
+        return g, (lambda: g(samples, targets, captions, cats))
+
     if use_graphs:
         # GEMM library inside the captured region (GDINO_GRAPH_BLAS: "hipblaslt"
         # or "cublas" = rocBLAS on ROCm)
         blas = os.environ.get("GDINO_GRAPH_BLAS")
         if blas:
             torch.backends.cuda.preferred_blas_library(blas)
-        from gdino_amd.stepgraph import TrainStepGraph
-        step_graph = TrainStepGraph(model, criterion, optimizer, grad_sync=grad_sync)
-        try:
-            step_graph(samples, targets, captions, cats)  # capture (+ its eager warm-up steps) and one replay
-            sync()
-            _progress("step graph captured and replayed once")
-        except Exception as e:  # capture refused: measure the eager step instead
-            step_graph.release()
-            step_graph = None
-            use_graphs = False
-            graph_note = f"graph capture failed, eager step measured: {repr(e)[:200]}"
-            print(f"warning: {graph_note}", file=sys.stderr, flush=True)
-        else:
-            def step():
-                return step_graph(samples, targets, captions, cats)
-
-    for _ in range(a.warmup):
-        step()
-    sync()
-    if world > 1:
-        dist.barrier()
-    _progress(f"{a.warmup} warm-up steps done")
+        # a capture failure on any rank sends EVERY rank to the eager step
+        # (TrainStepGraph's rank agreement); the line records each rank's mode
+        step_graph, step = make_graph_step()
+        step()  # capture (+ its rolled-back warm-up steps) and one replay
+        _bounded_sync(on_gpu, a.timeout, "first step (capture)")
+        _progress(f"step graph: {step_graph.stats()}")
 
     # MSDA launch timing over the timed region (eager); with graphs the
     # launches are inside the replays, where ROCm refuses timing events: they
     # are timed in the eager step that follows the timed region
     msda.timer = None if use_graphs else msda.LaunchTimer()
-    sync()
-    if world > 1:
-        dist.barrier()
-    # per-step device-side boundaries: one event per step on the current
-    # stream (no host sync inside the timed loop); the host clock brackets the
-    # whole region as the contract asks
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if on_gpu else None
-    host_marks = []
-    t0 = time.perf_counter()
-    if evs:
-        evs[0].record()
-    for i in range(a.steps):
-        loss = step()
-        if evs:
-            evs[i + 1].record()
-        host_marks.append(time.perf_counter())
-    sync()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if evs:
-        step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)]
-    else:
-        step_ms = [(b - a_) * 1e3 for a_, b in zip([t0] + host_marks[:-1], host_marks)]
-    step_stats = _dist_stats(step_ms)
+    elapsed, step_stats, loss_v = _timed(step, a, on_gpu, world, ctrl, "headline")
     kern = msda.timer.summary() if msda.timer is not None else {}
     msda.timer = None
-    if world > 1:
-        t = torch.tensor([elapsed], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-    loss_v = float(loss)
     _progress(f"{a.steps} timed steps done: {elapsed / a.steps * 1e3:.1f} ms/step")
+    graph_stats = step_graph.agree.gather(step_graph.stats()) if step_graph is not None else None
 
     # one extra step, outside the timed region, with HIP events around every
     # C-ABI call: device time per HIP entry point (all kernel families, not
@@ -433,6 +500,9 @@ def main(argv=None, device_type="cuda", child_script=None):
     # others blocked in the gradient all-reduce, and the extra step would
     # also move the weights)
     hip_calls = None
+    timed_note = ("HIP events on the launch stream in one eager step right after the timed graph replays (ROCm "
+                  "refuses timing events inside a graph capture)" if use_graphs else
+                  "HIP events on the launch stream over the timed region")
     if on_gpu and world == 1:
         if use_graphs:  # the extra step runs eagerly: every C-ABI call is a Python call
             msda.timer = msda.LaunchTimer()
@@ -448,26 +518,45 @@ def main(argv=None, device_type="cuda", child_script=None):
             _lib.call_timer = None
             msda.timer = None
         _progress("per-entry-point timing step done")
-
-    images = a.bs * world * a.steps
-    value = images / elapsed
-    # dominant MSDA launch = largest total time (graph mode: the launches of
-    # the last timed replay, via the capture's external timing events)
-    roofline = None
-    if kern:
-        kname, kd = max(kern.items(), key=lambda kv: kv[1]["ms"])
-        avg_s = kd["ms"] / kd["n"] * 1e-3
-        achieved = kd["bytes"] / avg_s
-        roofline = {"bound": "hbm", "kernel": f"msda_{kname[0]} (Lq={kname[1]})",
-                    "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK, "traffic": pmc_traffic(kname, a.bs),
-                    "avg_launch_us": avg_s * 1e6, "algo_bytes_per_launch": kd["bytes"],
-                    "timed": ("HIP events on the launch stream in one eager step right after the timed graph "
-                              "replays (ROCm refuses timing events inside a graph capture)" if use_graphs else
-                              "HIP events on the launch stream over the timed region")}
+    roofline = _roofline(kern, a.bs, timed_note)
     kernels = {f"msda_{k}_lq{lq}": {"launches": d["n"], "avg_us": d["ms"] / d["n"] * 1e3,
                                      "algo_bytes": d["bytes"], "GBps": d["bytes"] / (d["ms"] / d["n"] * 1e-3) / 1e9}
                for (k, lq), d in sorted(kern.items())}
+
+    # the reference's own configuration, measured in the same run: cfg_odvg's
+    # activation checkpointing (use_checkpoint / use_transformer_ckpt,
+    # config/cfg_odvg.py:41-42) recomputes the Swin blocks, fusion and
+    # encoder layers in the backward
+    ckpt_on = None
+    compare = a.ckpt_compare == "on" or (a.ckpt_compare == "auto" and use_graphs)
+    if compare and not a.forward_only and a.checkpointing == "off":
+        if step_graph is not None:
+            step_graph.release()
+        set_activation_checkpointing(core, True)
+        if use_graphs:
+            step_graph, step2 = make_graph_step()
+            step2()
+            _bounded_sync(on_gpu, a.timeout, "first checkpoint-on step (capture)")
+        else:
+            step2 = eager_step
+        e2, st2, loss2 = _timed(step2, a, on_gpu, world, ctrl, "checkpointing on")
+        kern2 = {}
+        if on_gpu and world == 1:
+            msda.timer = msda.LaunchTimer()
+            try:
+                eager_step()
+                kern2 = msda.timer.summary()
+            finally:
+                msda.timer = None
+        ckpt_on = {"activation_checkpointing": True, "value": a.bs * world * a.steps / e2,
+                   "ms_per_step": e2 / a.steps * 1e3, "step_ms": st2, "loss": loss2,
+                   "roofline": _roofline(kern2, a.bs, timed_note),
+                   "step_graph": step_graph.stats() if step_graph is not None else None}
+        set_activation_checkpointing(core, False)
+        _progress(f"checkpointing on: {ckpt_on['ms_per_step']:.1f} ms/step")
+
+    images = a.bs * world * a.steps
+    value = images / elapsed
 
     if a.output_dir and not a.forward_only:
         from gdino_amd import checkpoint as ckpt
@@ -477,8 +566,7 @@ def main(argv=None, device_type="cuda", child_script=None):
     if rank == 0:
         mode = "forward (eval, no autograd)" if a.forward_only else "train step (fwd+bwd+AdamW)"
         res = {
-            "metric": ("forward images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU" if a.forward_only else
-                       "train images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU"),
+            "metric": ("forward images/sec GroundingDINO-SwinT 800x1333 bs=2/GPU" if a.forward_only else METRIC),
             "value": value,
             "unit": "images/s",
             "n_gpus": world,
@@ -503,11 +591,14 @@ def main(argv=None, device_type="cuda", child_script=None):
             "roofline": roofline,
             "kernels": kernels,
             "hip_entry_points_one_step": hip_calls,
-            "options": {"hip_graphs": bool(use_graphs), "graph_note": graph_note, "tunableop": a.tunableop,
+            "options": {"hip_graphs": bool(use_graphs), "tunableop": a.tunableop,
                         "step_graph": ("whole train step (forward, device Hungarian matching + loss, backward, "
                                        "all-reduce, clip, AdamW) as one HIP graph" if use_graphs else None),
+                        # per rank: graph / eager mode, captures, replays, eager steps
+                        "step_graph_by_rank": graph_stats,
                         "grad_sync": (f"bucketed RCCL all-reduce overlapped with the backward (post-accumulate "
-                                      f"hooks, gradients as bucket views, captured in the step graph), buckets "
+                                      f"hooks, gradients as bucket views, buckets launched in index order, "
+                                      f"captured in the step graph), buckets "
                                       f"{[round(x, 1) for x in grad_sync.bucket_sizes_mb()]} MB"
                                       if grad_sync is not None else
                                       ("DDP (overlapped, eager step)" if world > 1 and not a.forward_only else None)),
@@ -517,6 +608,12 @@ def main(argv=None, device_type="cuda", child_script=None):
                         "msda_bwd": os.environ.get("GD_MSDA_BWD", "sorted")},
             "loss": loss_v,
         }
+        if ckpt_on is not None:
+            # the reference configuration (cfg_odvg: checkpointing on), same run
+            res["config"]["value_ckpt_on"] = ckpt_on["value"]
+            res["config"]["ms_per_step_ckpt_on"] = ckpt_on["ms_per_step"]
+            res["config"]["roofline_ckpt_on"] = ckpt_on["roofline"]
+            res["config"]["ckpt_on"] = ckpt_on
         if not math.isfinite(loss_v):
             res["error"] = f"non-finite loss {loss_v}: the step diverged, the throughput is not a valid measurement"
         if not a.no_cpu_baseline and world == 1:
@@ -529,10 +626,10 @@ def main(argv=None, device_type="cuda", child_script=None):
         # that references it aborts)
         if step_graph is not None:
             step_graph.release()
-        step = None
         import gc
         gc.collect()
-        sync()
+        _bounded_sync(on_gpu, a.timeout, "teardown")
+        _barrier(world, ctrl)
         dist.destroy_process_group()
     if not math.isfinite(loss_v):
         raise SystemExit(1)

@@ -213,6 +213,27 @@ def is_dist_avail_and_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+_LOCAL_ONLY = contextvars.ContextVar("gdino_local_only", default=False)
+
+
+@contextlib.contextmanager
+def local_only(flag: bool = True):
+    """Within: the train step issues no collective (the criterion's num_boxes
+    all-reduce is skipped, BucketedGradSync reduces nothing).  The step
+    graph's warm-up iterations run this way -- their effects on the weights
+    and the optimizer are rolled back afterwards -- so that a capture on one
+    rank never adds collectives the other ranks do not issue."""
+    tok = _LOCAL_ONLY.set(bool(flag))
+    try:
+        yield
+    finally:
+        _LOCAL_ONLY.reset(tok)
+
+
+def collectives_enabled() -> bool:
+    return is_dist_avail_and_initialized() and not _LOCAL_ONLY.get()
+
+
 def get_world_size() -> int:
     return dist.get_world_size() if is_dist_avail_and_initialized() else 1
 

@@ -18,7 +18,7 @@ from typing import List, Tuple
 
 import torch
 
-from .misc import NestedTensor
+from .misc import NestedTensor, collectives_enabled
 
 
 # ------------------------------------------------------------------ batches
@@ -201,41 +201,60 @@ class BucketedGradSync:
     INSIDE a captured HIP graph (gdino_amd.stepgraph), where DDP's own
     bookkeeping cannot follow replays.
 
-    * Buckets follow the order in which the backward finishes gradients
-      (recorded in the first backward, as DDP rebuilds its buckets after the
-      first iteration); a bucket holds up to ``bucket_mb`` of gradients, the
-      first one ``first_bucket_mb`` so the first collective starts early.
-    * Each trainable parameter's ``.grad`` is a view into its bucket's flat
+    * The bucket plan follows the order in which the backward finishes
+      gradients, recorded by one backward pass (DDP rebuilds its buckets
+      after the first iteration the same way).  Rank 0's recorded order is
+      broadcast and every rank builds the same buckets from it (DDP syncs
+      its rebuilt bucket indices with rank 0 too), so the ranks' bucket
+      sizes and order agree even where their batches take different paths.
+      A bucket holds up to ``bucket_mb`` of gradients, the first one
+      ``first_bucket_mb`` so the first collective starts early.
+    * Each bucketed parameter's ``.grad`` is a view into its bucket's flat
       buffer (DDP's gradient_as_bucket_view): the backward accumulates
       straight into the buffer, and there is no flatten / unflatten copy.
-    * A post-accumulate-grad hook counts a bucket's ready gradients; the last
-      one divides the bucket by the world size and issues its RCCL
-      all-reduce (async, on the process group's communication stream) while
-      the backward goes on producing the next buckets.  A callback at the end
-      of the backward waits for every bucket (the current stream waits on the
-      communication stream: no host block on the GPU).
+    * A post-accumulate-grad hook counts a bucket's ready gradients.  Buckets
+      are launched strictly in index order (a cursor, as DDP's reducer):
+      when bucket i fills, it and every following bucket that is full are
+      divided by the world size and all-reduced asynchronously (the process
+      group's communication stream) while the backward goes on.  Every rank
+      therefore issues the same collectives in the same order, whatever
+      order its gradients arrive in.  A callback at the end of the backward
+      launches what is left (in order) and waits for every bucket (the
+      current stream waits on the communication stream: no host block).
     * ``zero_grad()`` replaces optimizer.zero_grad(set_to_none=True), which
       would drop the views.
-    Same averaged gradients as DDP (tests/test_ddp_gloo.py).  Parameters that
-    receive no gradient in the recording backward keep ``.grad = None``."""
+    * Under ``misc.local_only()`` (the step graph's rolled-back warm-up
+      iterations) nothing is reduced.
+    ``control_group`` (optional, e.g. a gloo group): where rank 0's order is
+    broadcast; default the gradient group.  Same averaged gradients as DDP
+    (tests/test_ddp_gloo.py).  Parameters that receive no gradient in rank
+    0's recording backward keep ``.grad = None``."""
 
-    def __init__(self, params, bucket_mb: float = 25, first_bucket_mb: float = 1, group=None):
+    def __init__(self, params, bucket_mb: float = 25, first_bucket_mb: float = 1, group=None, control_group=None):
         import torch.distributed as dist
-        self.dist, self.group = dist, group
+        self.dist, self.group, self.control_group = dist, group, control_group
         self.world = dist.get_world_size(group)
         self.params = [p for p in params if p.requires_grad]
+        self.index = {id(p): i for i, p in enumerate(self.params)}
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.first_bytes = int(first_bucket_mb * (1 << 20))
         self.order = []          # grad-ready order seen by the recording backward
-        self.buckets = None      # [{"flat", "params", "pending", "work"}]
+        self.buckets = None      # [{"flat", "params", "pending", "work", "ready"}]
         self.bucket_of = {}
         self._queued = False
+        self._next = 0           # launch cursor: the first bucket not yet launched
         self._handles = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
+
+    @staticmethod
+    def _local():
+        return not collectives_enabled()
 
     # ---------------------------------------------------------------- hooks
     def _ready(self, p):
         if self.buckets is None:
             self.order.append(p)
+            return
+        if self._local():
             return
         if not self._queued:
             self._queued = True
@@ -245,32 +264,53 @@ class BucketedGradSync:
             return
         b["pending"] -= 1
         if b["pending"] == 0:
-            self._launch(b)
+            b["ready"] = True
+            self._launch_ready()
+
+    def _launch_ready(self):
+        while self._next < len(self.buckets) and self.buckets[self._next]["ready"]:
+            self._launch(self.buckets[self._next])
+            self._next += 1
 
     def _launch(self, b):
         b["flat"].div_(self.world)
         b["work"] = self.dist.all_reduce(b["flat"], group=self.group, async_op=True)
 
     def _finalize(self):
-        for b in self.buckets:
-            if b["work"] is None:  # a parameter without gradient this pass
-                self._launch(b)
+        for b in self.buckets:  # buckets with a parameter that got no gradient this pass
+            b["ready"] = True
+        self._launch_ready()
         for b in self.buckets:
             b["work"].wait()
             b["work"] = None
             b["pending"] = len(b["params"])
+            b["ready"] = False
+        self._next = 0
         self._queued = False
 
     # ------------------------------------------------------------ lifecycle
-    def _build(self):
-        """Buckets over the recorded order; grads move into the flat buffers."""
-        seen, order = set(), []
+    def _agreed_order(self):
+        """Rank 0's recorded order (parameter indices), broadcast to every
+        rank; a rank without a recording contributes nothing."""
+        seen, mine = set(), []
         for p in self.order:
             if id(p) not in seen and p.grad is not None:
                 seen.add(id(p))
-                order.append(p)
+                mine.append(self.index[id(p)])
+        self.order = []
+        if self.world == 1:
+            return mine
+        box = [mine]
+        self.dist.broadcast_object_list(box, src=self.dist.get_global_rank(self.group, 0)
+                                        if self.group is not None else 0, group=self.control_group or self.group)
+        return list(box[0])
+
+    def _build(self, order):
+        """Buckets over ``order`` (indices into self.params); existing grads
+        move into the flat buffers, missing ones start at zero."""
         self.buckets, cur, size = [], [], 0
-        for p in order:
+        for i in order:
+            p = self.params[i]
             nbytes = p.numel() * 4
             cap = self.first_bytes if not self.buckets else self.bucket_bytes
             if cur and (size + nbytes > cap or p.dtype != cur[0].dtype):
@@ -286,27 +326,50 @@ class BucketedGradSync:
             off = 0
             for p in ps:
                 view = flat[off:off + p.numel()].view_as(p)
-                view.copy_(p.grad)
+                if p.grad is not None:
+                    view.copy_(p.grad)
                 p.grad = view
                 off += p.numel()
-            b = {"flat": flat, "params": ps, "pending": len(ps), "work": None}
+            b = {"flat": flat, "params": ps, "pending": len(ps), "work": None, "ready": False}
             built.append(b)
             for p in ps:
                 self.bucket_of[id(p)] = b
         self.buckets = built
+        self._next = 0
 
-    def after_backward(self):
-        """Call after every backward (train_step does): the recording pass
-        all-reduces its gradients in one go and builds the buckets; later
-        passes were already reduced by the hooks."""
+    def plan(self, run_backward):
+        """Build the buckets from one recording backward ``run_backward()``
+        (forward + backward, no optimizer step; run under local_only by the
+        caller).  Every rank calls this exactly once, also when its
+        recording fails (it then takes rank 0's order)."""
         if self.buckets is not None:
             return
-        self._build()
+        try:
+            run_backward()
+        except Exception:
+            self.order = []
+            raise
+        finally:
+            order = self._agreed_order()
+            self._build(order)
+
+    def after_backward(self):
+        """Call after every backward (train_step does): the first, recording
+        pass builds the buckets from rank 0's order and all-reduces them in
+        one go; later passes were already reduced by the hooks."""
+        if self.buckets is not None:
+            return
+        self._build(self._agreed_order())
+        if self._local():
+            return
         for b in self.buckets:
-            self._launch(b)
+            b["ready"] = True
+        self._launch_ready()
         for b in self.buckets:
             b["work"].wait()
             b["work"] = None
+            b["ready"] = False
+        self._next = 0
 
     def zero_grad(self):
         if self.buckets is None:

@@ -36,7 +36,7 @@ from torch import nn
 
 from gdino_amd import box_ops, castcache
 from gdino_amd.conv import GemmConv2d
-from gdino_amd.misc import (NestedTensor, box_refine, no_padding, get_world_size,
+from gdino_amd.misc import (NestedTensor, box_refine, collectives_enabled, no_padding, get_world_size,
                             is_dist_avail_and_initialized,
                             nested_tensor_from_tensor_list)
 from gdino_amd.tokenizer import get_pretrained_language_model, get_tokenlizer
@@ -67,6 +67,36 @@ def prepare_text_host(tokenizer, special_tokens, max_text_len, captions):
             "text_token_mask": tok["attention_mask"].bool(), "self_masks": self_masks,
             "position_ids": position_ids}
     return text, tokenized
+
+
+def pad_text(text: dict, multiple: int, max_text_len: int) -> dict:
+    """prepare_text_host's tensors with T padded to a multiple of
+    ``multiple`` (at most max_text_len) by pad tokens, as the tokenizer's
+    padding itself produces them: id 0, type 0, attention-mask False,
+    position id 0 and a phrase-mask row / column that holds only the pad
+    token's own diagonal entry (bertwarper.py:224-273 builds the blocks from
+    the special tokens; tokens after the last one attend only to
+    themselves).  No real token attends to a pad token anywhere (BERT's
+    phrase masks, the text enhancer, BiAttention and the decoder's text
+    cross-attention mask them, the contrastive head writes -inf), so every
+    output of a real token is unchanged.  The step graph pads T this way so
+    that batches of different caption lengths share a graph."""
+    T = text["input_ids"].shape[1]
+    Tb = min(max(-(-T // max(multiple, 1)) * max(multiple, 1), T), max(max_text_len, T))
+    if Tb == T:
+        return text
+    pad = Tb - T
+    out = {}
+    for k in ("input_ids", "token_type_ids", "position_ids"):
+        out[k] = torch.nn.functional.pad(text[k], (0, pad), value=0)
+    out["text_token_mask"] = torch.nn.functional.pad(text["text_token_mask"], (0, pad), value=False)
+    m = text["self_masks"]
+    sm = torch.zeros(m.shape[0], Tb, Tb, dtype=m.dtype)
+    sm[:, :T, :T] = m
+    idx = torch.arange(T, Tb)
+    sm[:, idx, idx] = True
+    out["self_masks"] = sm
+    return out
 
 
 _STAGING = []  # (pinned host buffer, event recorded after its copy)
@@ -184,15 +214,18 @@ class GroundingDINO(nn.Module):
         self.refpoint_embed = nn.Embedding(use_num_queries, self.query_dim)
 
     # ------------------------------------------------------------------ text
-    def prepare_text(self, captions, device, prepared=None):
+    def prepare_text(self, captions, device, prepared=None, pad_multiple=1):
         """Host side of the text path (tokenize, phrase masks / position ids,
         truncate to max_text_len: prepare_text_host) and one move to the
         device.  ``prepared`` = prepare_text_host's result computed elsewhere
         (e.g. in DataLoader workers by gdino_amd.data.TextPreprocessor);
-        pinned tensors are copied asynchronously.
+        pinned tensors are copied asynchronously.  ``pad_multiple`` > 1: T
+        padded to a multiple of it (pad_text).
         -> (dict of device tensors, tokenizer output for the loss)."""
         text, tokenized = prepared if prepared is not None else prepare_text_host(
             self.tokenizer, self.specical_tokens, self.max_text_len, captions)
+        if pad_multiple > 1:
+            text = pad_text(text, pad_multiple, self.max_text_len)
         return {k: to_device_async(v, device) for k, v in text.items()}, tokenized
 
     def encode_text(self, input_ids, token_type_ids, text_token_mask, self_masks, position_ids):
@@ -389,7 +422,7 @@ class SetCriterion(nn.Module):
                               .to(device))
 
         num_boxes = torch.as_tensor([float(sum(len(t["labels"]) for t in targets))], device=device)
-        if is_dist_avail_and_initialized():
+        if collectives_enabled():
             torch.distributed.all_reduce(num_boxes)
         num_boxes = torch.clamp(num_boxes / get_world_size(), min=1)[0]
 
@@ -470,7 +503,7 @@ class SetCriterion(nn.Module):
         K = maps.shape[1]
 
         num_boxes = prep["num_boxes"].clone()
-        if is_dist_avail_and_initialized():
+        if collectives_enabled():
             torch.distributed.all_reduce(num_boxes)
         num_boxes = torch.clamp(num_boxes / get_world_size(), min=1)[0]
 

@@ -52,14 +52,12 @@ def main():
         def zero_grad(self, set_to_none=True):
             model.zero_grad(set_to_none=set_to_none)
 
-    g = TrainStepGraph.__new__(TrainStepGraph)
-    g.model, g.criterion, g.optimizer = model, crit, NoStep()
-    g.clip_max_norm, g.amp_dtype, g.grad_sync, g.kmax_multiple = 0.1, torch.bfloat16, None, 8
+    g = TrainStepGraph(model, crit, NoStep(), clip_max_norm=0.1, amp_dtype=torch.bfloat16)
     b = synthetic_batch(2, a.height, a.width, n_boxes=a.boxes, n_tokens=a.tokens, seed=11, device="cpu")
     t0 = time.time()
     with emulated_product():
-        inputs = g._prepare(*b)
-        loss, _ = g._body(inputs, True)
+        inputs, pf = g._prepare(*b)
+        loss, _ = g._body(inputs, pf)
     print(f"emu step: loss {float(loss):.4f} in {time.time() - t0:.0f} s", flush=True)
     print("emu-step-ok", flush=True)
 

@@ -35,3 +35,32 @@ def oracle_msda():
             yield
     finally:
         mod.MSDeformAttnFunction = prev
+
+
+@contextlib.contextmanager
+def scipy_lsap():
+    """Route the device Hungarian solver (gdino_amd.lsap, csrc/lsap.hip) to
+    scipy's linear_sum_assignment -- the reference's own solver and the
+    kernel's oracle -- so SetCriterion.loss_prepared runs on CPU tensors."""
+    import numpy as np
+    import torch
+    from scipy.optimize import linear_sum_assignment
+
+    from gdino_amd import lsap
+
+    def host(cost, sizes, status=None):
+        p, q, k = cost.shape
+        rows = torch.full((p, k), -1, dtype=torch.int64)
+        cols = torch.full((p, k), -1, dtype=torch.int64)
+        c = cost.detach().double().cpu().numpy()
+        for i, n in enumerate(sizes.tolist()):
+            r, cc = linear_sum_assignment(np.asarray(c[i, :, :n]))
+            rows[i, :len(r)], cols[i, :len(r)] = torch.from_numpy(r), torch.from_numpy(cc)
+        return rows.to(cost.device), cols.to(cost.device)
+
+    saved = lsap.linear_sum_assignment_batched
+    lsap.linear_sum_assignment_batched = host
+    try:
+        yield
+    finally:
+        lsap.linear_sum_assignment_batched = saved

@@ -257,3 +257,117 @@ def test_decoder_ffn_grads_in_a_graph(autocast):
             if d > 1e-5:
                 bad.append((n, d, p.grad.reshape(-1)[:3].tolist(), ref[n].reshape(-1)[:3].tolist()))
     assert not bad, bad
+
+
+def test_capture_step_applies_the_batch_once():
+    """the capture's warm-up iterations are rolled
+    back, so the first TrainStepGraph call moves the weights by ONE AdamW
+    step, like one eager step (an un-rolled-back warm-up would apply three:
+    the update vector's norm about twice or three times the eager one)."""
+    from gdino_amd.stepgraph import TrainStepGraph
+    from gdino_amd.train import train_step
+    b = _batch(21, 4)
+    upd = {}
+    for mode in ("eager", "eager2", "graph"):
+        model, crit, opt = _model()
+        p0 = _params(model)
+        if mode == "graph":
+            g = TrainStepGraph(model, crit, opt, warmup=2)
+            g(*b)
+            assert g.stats()["captures"] == 1 and g.stats()["replays"] == 1
+        else:
+            train_step(model, crit, opt, *b)
+        torch.cuda.synchronize()
+        upd[mode] = _params(model) - p0
+        steps = {float(s["step"]) for s in opt.state.values()}
+        assert steps == {1.0}, (mode, steps)
+    noise = float((upd["eager2"] - upd["eager"]).norm() / upd["eager"].norm())
+    d = float((upd["graph"] - upd["eager"]).norm() / upd["eager"].norm())
+    assert d <= max(0.05, 3 * noise), (d, noise)
+
+
+def test_step_graph_cache_on_a_stream_of_batches():
+    """a stream of odvg-style batches
+    with 11 distinct caption lengths, 3 image sizes and 1-8 boxes runs on at
+    most 4 captured graphs (text padded to 64-token buckets, images to
+    64-px buckets, targets to 8 slots); the graphs share one memory pool, so
+    reserved HBM stays flat once the cache is warm; every step's loss and
+    gradients equal an eager step on the same (bucketed) batch within the
+    eager run-to-run spread."""
+    from gdino_amd.stepgraph import TrainStepGraph
+    from gdino_amd.train import synthetic_batch
+    sizes = [(320, 384), (300, 370), (256, 320)]
+    tokens = [12, 18, 24, 30, 36, 44, 52, 60, 70, 90, 110]
+    stream = []
+    for i in range(14):
+        h, w = sizes[i % 3]
+        stream.append(synthetic_batch(2, h, w, n_boxes=1 + (i * 3) % 8, n_tokens=tokens[i % len(tokens)],
+                                      seed=300 + i, device=DEV))
+    runs = {}
+    for mode in ("graph", "eager", "eager2"):
+        model, crit, opt = _model()
+        for grp in opt.param_groups:
+            grp["lr"], grp["weight_decay"] = 0.0, 0.0
+        kw = dict(warmup=1, text_multiple=64, image_multiple=64)
+        if mode == "graph":
+            g = TrainStepGraph(model, crit, opt, max_graphs=4, capture_after=2, **kw)
+        else:
+            g = TrainStepGraph(model, crit, opt, max_graphs=0, capture_after=10 ** 9, **kw)
+        out, reserved = [], []
+        for b in stream:
+            loss = float(g(*b))
+            out.append((loss, _grads(model)))
+            torch.cuda.synchronize()
+            reserved.append(torch.cuda.memory_reserved())
+        runs[mode] = (out, reserved, g.stats())
+        del model, crit, opt, g
+    st = runs["graph"][2]
+    assert st["mode"] == "graph" and 1 <= st["captures"] <= 4 and st["replays"] + st["eager_steps"] == len(stream), st
+    assert st["replays"] >= len(stream) - st["captures"] - 2, st
+    res = {"eager": runs["eager"][0], "eager2": runs["eager2"][0], "graph": runs["graph"][0]}
+    _check(res)
+    rg = runs["graph"][1]
+    warm = rg[len(stream) // 2]
+    assert rg[-1] <= warm * 1.05 + (256 << 20), (rg, st)
+
+
+def test_failed_capture_falls_back_to_the_eager_step():
+    """A capture that fails in the middle of the forward -- inside a
+    checkpointed Swin block, where a host synchronisation is refused while
+    the stream captures -- leaves the step graph in eager mode, and its
+    eager steps give the eager train step's losses and gradients (the
+    aborted capture's checkpoint hooks must not leak into them)."""
+    from gdino_amd.stepgraph import TrainStepGraph
+    from gdino_amd.train import train_step
+    CKPT[0] = True
+    try:
+        b1, b2 = _batch(11, 5), _batch(12, 3)
+        res = {}
+        for mode in ("eager", "eager2", "graph"):
+            model, crit, opt = _model()
+            for grp in opt.param_groups:
+                grp["lr"], grp["weight_decay"] = 0.0, 0.0
+            out = []
+            if mode == "graph":
+                blk = model.backbone[0].layers[0].blocks[0]
+                orig = blk.forward
+
+                def bad(*a, _orig=orig, **k):
+                    if torch.cuda.is_current_stream_capturing():
+                        torch.cuda.synchronize()  # refused during capture
+                    return _orig(*a, **k)
+                blk.forward = bad
+                g = TrainStepGraph(model, crit, opt, warmup=1)
+                for b in (b1, b2):
+                    out.append((float(g(*b)), _grads(model)))
+                st = g.stats()
+                assert st["mode"] == "eager" and st["captures"] == 0 and st["eager_steps"] == 2, st
+                assert "capturing" in (st["fallback_reason"] or ""), st
+            else:
+                for b in (b1, b2):
+                    out.append((float(train_step(model, crit, opt, *b)), _grads(model)))
+            torch.cuda.synchronize()
+            res[mode] = out
+        _check(res)
+    finally:
+        CKPT[0] = True

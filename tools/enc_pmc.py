@@ -1,5 +1,5 @@
-"""Encoder-shape MSDA forward and backward (bs=2, 800x1333, bf16, init
-geometry), a few launches each: the program rocprofv3 --pmc runs to read the
+"""Encoder-shape MSDA forward and backward (bs=2, 800x1333, bf16 value and
+grad_value as the model calls it, init geometry), a few launches each: the program rocprofv3 --pmc runs to read the
 SQ counters of the two kernels (tools/gpu_enc_pmc.sh)."""
 import os
 import sys
@@ -16,7 +16,7 @@ v, sh, ls, loc, attn, go = mb.inputs(S, torch.bfloat16)
 loc = mb.init_geometry_loc(2)
 for _ in range(3):
     msda.ms_deform_attn_forward(v, sh, ls, loc, attn, 64)
-    msda.ms_deform_attn_backward(v, sh, ls, loc, attn, go, 64, grad_value_dtype=torch.float32,
+    msda.ms_deform_attn_backward(v, sh, ls, loc, attn, go, 64, grad_value_dtype=torch.bfloat16,
                                  host_shapes=mb.LEVELS)
 torch.cuda.synchronize()
 print("enc_pmc done")

@@ -121,6 +121,28 @@ graphs)
   GDINO_GRAPH_DEBUG=1 T 600 python3 bench.py --no-cpu-baseline --graphs --steps 5 --warmup 2 \
       > gpurun_out/s_bench_graphs.log 2>&1
   ;;
+msdapmc)
+  # encoder-shape MSDA kernels alone: timings per variant, then FETCH_SIZE
+  # and WRITE_SIZE in separate --pmc passes over tools/enc_pmc.py
+  step "msda microbench (sorted backward, encoder shapes)" &&
+  T 300 python3 tools/msda_microbench.py --bwd-variants --variant sorted > gpurun_out/s_msda_bwd.jsonl 2>&1 &&
+  step "pmc FETCH_SIZE" &&
+  T 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex "msda|scan|fill" --output-format csv \
+      -d "$PROF/m_fetch" -o run -- python3 tools/enc_pmc.py > gpurun_out/s_pmc_fetch.log 2>&1 &&
+  step "pmc WRITE_SIZE" &&
+  T 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --kernel-include-regex "msda|scan|fill" --output-format csv \
+      -d "$PROF/m_write" -o run -- python3 tools/enc_pmc.py > gpurun_out/s_pmc_write.log 2>&1 &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/m_fetch" --write "$PROF/m_write" \
+      --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
+  ;;
+syncab)
+  # the driver's bench command with the device-wide sync after each replay and
+  # with the event-bounded replay queue
+  step "bench (device sync)" &&
+  GDINO_STEPGRAPH_SYNC=device T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_bench_device.log 2>&1 &&
+  step "bench (event-bounded)" &&
+  GDINO_STEPGRAPH_SYNC=event T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_bench_event.log 2>&1
+  ;;
 *)
   echo "usage: $0 [tests|bench|core|prof|tune|ab|graphs]" >&2
   exit 2

@@ -146,11 +146,9 @@ def whole_step(a):
         def zero_grad(self, set_to_none=True):
             model.zero_grad(set_to_none=set_to_none)
 
-    g = TrainStepGraph.__new__(TrainStepGraph)
-    g.model, g.criterion, g.optimizer = model, criterion, NoStep()
     on_gpu = dev.type == "cuda"
     # on the GPU the product path itself (bf16 autocast, the device LSA)
-    g.clip_max_norm, g.amp_dtype, g.grad_sync, g.kmax_multiple = 0.1, (torch.bfloat16 if on_gpu else None), None, 8
+    g = TrainStepGraph(model, criterion, NoStep(), clip_max_norm=0.1, amp_dtype=torch.bfloat16 if on_gpu else None)
     samples, targets, captions, cats = synthetic_batch(2, a.height, a.width, n_boxes=4, n_tokens=64, seed=0,
                                                        device=dev)
     saved = lsap.linear_sum_assignment_batched
@@ -159,10 +157,10 @@ def whole_step(a):
     import contextlib
     try:
         with (contextlib.nullcontext() if on_gpu else oracle_msda()):
-            inputs = g._prepare(samples, targets, captions, cats)
-            g._body(inputs)  # warm-up: device constants, caches
+            inputs, pf = g._prepare(samples, targets, captions, cats)
+            g._body(inputs, pf)  # warm-up: device constants, caches
             with audit:
-                g._body(inputs)
+                g._body(inputs, pf)
     finally:
         lsap.linear_sum_assignment_batched = saved
     if not audit.hits:
