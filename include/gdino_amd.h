@@ -105,6 +105,7 @@ typedef enum {
   GD_ERR_INVALID = 1,     /* bad argument (shape, null pointer, dtype) */
   GD_ERR_UNSUPPORTED = 2, /* valid but not implemented combination */
   GD_ERR_LAUNCH = 3,      /* HIP launch / runtime error */
+  GD_ERR_DEVICE = 4,      /* a device-side check failed (gd_device_status) */
 } gd_status;
 
 typedef enum {
@@ -488,6 +489,13 @@ gd_status gd_linear_sum_assignment(const float* cost, int problems, int Q, int K
 const char* gd_last_error(void);
 /* "hip=<runtime version>;arch=<gcnArchName of current device>;build=<hipcc>" */
 const char* gd_runtime_info(void);
+/* Synchronises `stream`, then reads and clears the library's device-side
+ * check word: GD_OK, or GD_ERR_DEVICE with the failed check in
+ * gd_last_error().  The kernels never store out of bounds when a check fails
+ * (e.g. the sorted MSDA backward drops a record whose slot lies past its
+ * buffer instead of faulting); this call is how the host learns of it.
+ * Not for use inside a graph capture (it synchronises). */
+gd_status gd_device_status(gd_stream_t stream);
 /* ABI version: bumped when a signature changes. */
 int gd_abi_version(void);
 

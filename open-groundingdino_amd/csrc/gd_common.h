@@ -50,6 +50,13 @@ inline hipStream_t as_hip(gd_stream_t s) { return reinterpret_cast<hipStream_t>(
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+// c + a.lo * b.lo + a.hi * b.hi for two packed bf16 pairs: one
+// v_dot2c_f32_bf16 (the bf16 products are exact in fp32) instead of two
+// unpacks and two FMAs per channel pair
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
+  typedef __bf16 gd_bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gd_bf16x2, a), __builtin_bit_cast(gd_bf16x2, b), c, false);
+}
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);

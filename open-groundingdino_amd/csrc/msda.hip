@@ -44,6 +44,11 @@
 
 namespace gd {
 namespace {
+// Device-side check word of the MSDA kernels (gd_device_status): a bit per
+// check, set with a vector atomic OR, read and cleared by the host.
+__device__ int g_device_err;
+constexpr int kErrMsdaSlot = 1;  // a sorted-backward record slot past the record buffer
+__device__ __forceinline__ void flag_device_error(int code) { atomicOr(&g_device_err, code); }
 #include "msda_kernels.inc"
 #include "msda_enc.inc"
 #include "msda_sorted.inc"
@@ -150,6 +155,13 @@ extern "C" gd_status gd_msda_forward(gd_dtype dt, const void* value,
     if (sb == 8) GD_FWD_LAUNCH(float, 8); else if (sb == 40) GD_FWD_LAUNCH(float, 40);
     else if (sb == 80) GD_FWD_LAUNCH(float, 80); else GD_FWD_LAUNCH(float, 4);
     GD_LAUNCH_CHECK("msda_fwd_vec<f32>");
+  } else if (dt == GD_BF16 && vec_ok && env_int("GD_MSDA_FWD_GS", 1) == 1) {
+    // geometry shared across the unit's quad + packed fp32 math (round 5);
+    // GD_MSDA_FWD_GS=0: msda_fwd_vec (A/B)
+    const int blocks = int((units + 63) / 64);
+    hipLaunchKernelGGL(msda_fwd_gs, dim3(blocks), dim3(256), 0, s, (const uint16_t*)value, shapes, lsi,
+                       (const float*)loc, (const float*)attn, (uint16_t*)out, S, Lq, M, int(units));
+    GD_LAUNCH_CHECK("msda_fwd_gs");
   } else if (dt == GD_BF16 && vec_ok) {
     constexpr int UPW = 64 / (32 / 8);
     const int blocks = int((units + 4 * UPW - 1) / (4 * UPW));
@@ -575,7 +587,14 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
       // on a 2-px spread (profiles/r03g); GD_MSDA_SORTED_LL=0: all 48
       // location / weight floats held from the start
       const bool ll = env_int("GD_MSDA_SORTED_LL", 1) == 1;
-      if (dt == GD_BF16) {
+      // bf16, heads in pairs: the geometry-shared kernel (round 5;
+      // GD_MSDA_SORTED_GS=0: msda_bwd_samples<.., 2, true>, A/B)
+      const bool gs = dt == GD_BF16 && hp && !pipe && ll && env_int("GD_MSDA_SORTED_GS", 1) == 1;
+      if (gs) {
+        hipLaunchKernelGGL(msda_bwd_samples_gs, dim3(pl.k1_blocks), dim3(256), 0, s, (const uint16_t*)value,
+                           (const float*)loc, (const float*)attn, (const uint16_t*)grad_out, (float*)grad_loc,
+                           (float*)grad_attn, cur, ids, pl.G, S, Lq, M, units, kpriv ? (const int*)stat : nullptr);
+      } else if (dt == GD_BF16) {
         if (pipe) GD_K1(uint16_t, true, 1, false);
         else if (hp && ll) GD_K1(uint16_t, false, 2, true);
         else if (hp) GD_K1(uint16_t, false, 2, false);
@@ -646,4 +665,17 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
 #undef GD_K4B
   GD_LAUNCH_CHECK("msda_bwd_pixsum");
   return GD_OK;
+}
+
+extern "C" gd_status gd_device_status(gd_stream_t stream) {
+  GD_HIP_CHECK(hipStreamSynchronize(as_hip(stream)));
+  int v = 0;
+  GD_HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(gd::g_device_err), sizeof(int), 0, hipMemcpyDeviceToHost));
+  if (v == 0) return GD_OK;
+  const int zero = 0;
+  GD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(gd::g_device_err), &zero, sizeof(int), 0, hipMemcpyHostToDevice));
+  gd::set_error("device-side check failed (bits 0x%x): %s", v,
+            (v & gd::kErrMsdaSlot) ? "msda sorted backward: a record slot past the record buffer (stale or "
+                                     "corrupt cell counts); the record was not stored" : "unknown check");
+  return GD_ERR_DEVICE;
 }

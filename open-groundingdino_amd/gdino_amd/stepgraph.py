@@ -212,6 +212,7 @@ class TrainStepGraph:
         self.captures = self.replays = self.eager_steps = self.evictions = 0
         self.mode = "graph"
         self.fallback_reason = None
+        self.last_terms = None
         self.agree = Agreement(control_group)
         self.device = next(model.parameters()).device
         self.on_gpu = self.device.type == "cuda"
@@ -239,12 +240,14 @@ class TrainStepGraph:
                 "fallback_reason": self.fallback_reason}
 
     # ------------------------------------------------------------ inputs
-    def _prepare(self, samples, targets, captions, cat_lists):
-        """-> (static-shape input dict on the device, padding_free)"""
+    def _prepare(self, samples, targets, captions, cat_lists, prepared_text=None):
+        """-> (static-shape input dict on the device, padding_free).
+        ``prepared_text``: prepare_text_host's result made in a DataLoader
+        worker (gdino_amd.data.ODVGCollator), else tokenised here."""
         model = self.model
         images, mask, pf = pad_images(samples, self.image_multiple)
         device = images.device
-        text, token = model.prepare_text(captions, device, pad_multiple=self.text_multiple)
+        text, token = model.prepare_text(captions, device, prepared=prepared_text, pad_multiple=self.text_multiple)
         k = max(max((len(t["labels"]) for t in targets), default=0), 1)
         k = -(-k // self.kmax_multiple) * self.kmax_multiple
         prep = self.criterion.prepare_targets(targets, cat_lists, captions, token, device, kmax=k)
@@ -457,8 +460,9 @@ class TrainStepGraph:
         if self.grad_sync is None:
             self.optimizer.zero_grad(set_to_none=True)
             self._grads_of = None
-        loss, _ = self._body(inputs, padding_free)
+        loss, terms = self._body(inputs, padding_free)
         self.eager_steps += 1
+        self.last_terms = terms
         return loss
 
     def _to_eager(self, reason):
@@ -486,8 +490,8 @@ class TrainStepGraph:
             self._inflight.append(ev)
 
     # -------------------------------------------------------------- call
-    def __call__(self, samples, targets, captions, cat_lists):
-        inputs, pf = self._prepare(samples, targets, captions, cat_lists)
+    def __call__(self, samples, targets, captions, cat_lists, prepared_text=None):
+        inputs, pf = self._prepare(samples, targets, captions, cat_lists, prepared_text)
         # at most max_inflight replays queued: this step's host preparation
         # above overlapped the previous replay
         while len(self._inflight) >= self.max_inflight:
@@ -539,6 +543,7 @@ class TrainStepGraph:
                     p.grad = g
                 self._grads_of = c
             loss = c.loss_out
+            self.last_terms = c.dict_out
             castcache._on_optimizer_step()  # the replay stepped the optimizer: cast copies are stale
         self._after_replay()
         if _VERBOSE and self.on_gpu:
@@ -547,9 +552,9 @@ class TrainStepGraph:
         return loss
 
     def loss_dict(self):
-        """The last replayed graph's loss terms (device tensors), or None."""
-        c = next(reversed(self.graphs.values()), None)
-        return None if c is None else c.dict_out
+        """The last step's loss terms (device tensors; a replayed graph's are
+        rewritten by its next replay), or None before the first step."""
+        return self.last_terms
 
     def release(self):
         self._drain()

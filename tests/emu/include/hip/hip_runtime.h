@@ -84,6 +84,17 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
   memset(p, v, n);
   return hipSuccess;
 }
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+constexpr int hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2;
+#define HIP_SYMBOL(x) (&(x))
+inline hipError_t hipMemcpyFromSymbol(void* dst, const void* sym, size_t n, size_t off = 0, int = 0) {
+  std::memcpy(dst, static_cast<const char*>(sym) + off, n);
+  return hipSuccess;
+}
+inline hipError_t hipMemcpyToSymbol(const void* sym, const void* src, size_t n, size_t off = 0, int = 0) {
+  std::memcpy(const_cast<char*>(static_cast<const char*>(sym)) + off, src, n);
+  return hipSuccess;
+}
 inline hipError_t hipRuntimeGetVersion(int* v) {
   *v = 0;
   return hipSuccess;
@@ -307,6 +318,13 @@ inline float bf16_bits_to_f(uint16_t h) {
 // lane l holds A[l&15][8(l>>4)+j] and B[8(l>>4)+j][l&15] in element j, and
 // receives D[4(l>>4)+r][l&15] in element r.  Products are exact; the sum is
 // taken in double and rounded once.
+// v_dot2c_f32_bf16: the two bf16 products are exact in fp32; modelled as
+// the sum of both products and c in double rounded once to fp32
+template <typename V2>
+inline float fdot2_bf16(V2 a, V2 b, float c) {
+  return float(double(float(a[0])) * double(float(b[0])) + double(float(a[1])) * double(float(b[1])) + double(c));
+}
+
 template <typename V8, typename C4>
 inline C4 mfma_16x16x32_bf16(V8 a, V8 b, C4 c) {
   static_assert(sizeof(V8) == 16 && sizeof(C4) == 16, "bf16x8 / f32x4 operands");
@@ -388,8 +406,10 @@ inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 #define __builtin_amdgcn_ds_swizzle(v, pattern) ::gd_emu::ds_swizzle((v), (pattern))
 #define __builtin_amdgcn_update_dpp(old, src, ctrl, rm, bm, bc) \
   ::gd_emu::update_dpp((old), (src), (ctrl), (rm), (bm), (bc))
+#define __builtin_amdgcn_mov_dpp(src, ctrl, rm, bm, bc) ::gd_emu::update_dpp((src), (src), (ctrl), (rm), (bm), (bc))
 #define __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, cbsz, abid, blgp) \
   ::gd_emu::mfma_16x16x32_bf16((a), (b), (c))
+#define __builtin_amdgcn_fdot2_f32_bf16(a, b, c, clamp) ::gd_emu::fdot2_bf16((a), (b), (c))
 #define __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, cbsz, abid, blgp) ::gd_emu::mfma_16x16x4_f32((a), (b), (c))
 #define hipLaunchKernelGGL(kernel, g, b, shm, stream, ...) \
   ((void)(shm), (void)(stream), ::gd_emu::launch(dim3(g), dim3(b), [&]() { kernel(__VA_ARGS__); }))
@@ -398,6 +418,13 @@ template <typename T>
 inline T atomicAdd(T* p, T v) {
   const T old = *p;
   *p = old + v;
+  return old;
+}
+
+template <typename T>
+inline T atomicOr(T* p, T v) {
+  const T old = *p;
+  *p = old | v;
   return old;
 }
 

@@ -933,3 +933,31 @@ def test_emulated_add_scaled(n, c, bd, sshape, sd, xd, monkeypatch):
             tol = 1e-4 if s.dtype == torch.float32 else 1e-2
         err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
         assert err <= tol, (name, err)
+
+
+@pytest.mark.parametrize("local,outliers", [(True, 0.1), (False, 0.0)])
+def test_emulated_geometry_shared_kernels_match_per_lane_kernels(local, outliers, monkeypatch):
+    """Round 5: the bf16 forward (msda_fwd_gs) and the sorted backward's
+    per-sample pass (msda_bwd_samples_gs) compute each sample's geometry on
+    one lane of the unit's quad and broadcast it by DPP; their results equal
+    the per-lane kernels' (msda_fwd_vec, msda_bwd_samples<.., 2, true>) up to
+    the summation rounding of the packed / dot2 arithmetic, including
+    locations outside the levels and NaN / inf locations."""
+    S = sum(h * w for h, w in MEDIUM)
+    value, shapes, lsi, loc, attn, grad_out = _levels_inputs(MEDIUM, 2, S if local else 41, seed=31,
+                                                             vdtype=torch.bfloat16, local=local,
+                                                             outlier_frac=outliers)
+    loc = loc.clone()
+    loc.view(-1)[::97] = float("nan")
+    loc.view(-1)[5::101] = float("inf")
+    res = {}
+    for gs in ("0", "1"):
+        monkeypatch.setenv("GD_MSDA_FWD_GS", gs)
+        monkeypatch.setenv("GD_MSDA_SORTED_GS", gs)
+        out = E.msda_forward(value, shapes, lsi, loc, attn)
+        gv, gl, ga = E.msda_backward_sorted(value, shapes, lsi, loc, attn, grad_out, host_shapes=MEDIUM)
+        res[gs] = (out.float(), gv.float(), gl, ga)
+    for a, b, name in zip(res["0"], res["1"], ("out", "grad_value", "grad_loc", "grad_attn")):
+        assert torch.isfinite(b).all(), name
+        assert E.rel_err(b.double().numpy(), a.double().numpy()) < (1e-2 if name in ("out", "grad_value") else 1e-5), \
+            (name, E.rel_err(b.double().numpy(), a.double().numpy()))

@@ -408,6 +408,7 @@ def test_sorted_level_loaded_locations_are_bitwise_the_default(geometry, monkeyp
     three gradients are bitwise equal."""
     monkeypatch.setenv("GD_MSDA_BWD", "sorted")
     monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "1")
+    monkeypatch.setenv("GD_MSDA_SORTED_GS", "0")  # the two per-lane-geometry variants
     value, shapes, lsi, loc, attn, grad_out = _encoder_inputs(LEVELS_800, 2, seed=43, vdtype=torch.bfloat16,
                                                               outlier_frac=0.02)
     if geometry == "init":
@@ -419,6 +420,33 @@ def test_sorted_level_loaded_locations_are_bitwise_the_default(geometry, monkeyp
         runs.append(_msda().ms_deform_attn_backward(*inputs, 64, host_shapes=LEVELS_800))
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("geometry", ["init", "spread"])
+def test_geometry_shared_kernels_match_the_per_lane_kernels(geometry, monkeypatch):
+    """Round 5: msda_fwd_gs and msda_bwd_samples_gs (one lane's geometry per
+    sample, DPP quad broadcasts, packed / dot2 arithmetic) against the
+    per-lane kernels on the 800x1333 encoder shape: forward and grad_value
+    within bf16 rounding, grad_loc / grad_attn within fp32 summation order
+    (deterministic mode, so grad_value's order is fixed)."""
+    monkeypatch.setenv("GD_MSDA_BWD", "sorted")
+    monkeypatch.setenv("GD_MSDA_DETERMINISTIC", "1")
+    value, shapes, lsi, loc, attn, grad_out = _encoder_inputs(LEVELS_800, 2, seed=47, vdtype=torch.bfloat16,
+                                                              outlier_frac=0.02)
+    if geometry == "init":
+        loc = _init_geometry_loc(LEVELS_800, 2)
+    inputs = [t.to(DEV) for t in (value, shapes, lsi, loc, attn, grad_out)]
+    res = {}
+    for gs in ("0", "1"):
+        monkeypatch.setenv("GD_MSDA_FWD_GS", gs)
+        monkeypatch.setenv("GD_MSDA_SORTED_GS", gs)
+        out = _msda().ms_deform_attn_forward(*inputs[:5], 64)
+        res[gs] = (out,) + tuple(_msda().ms_deform_attn_backward(*inputs, 64, host_shapes=LEVELS_800))
+    for i, (a, b) in enumerate(zip(res["0"], res["1"])):
+        a, b = a.float(), b.float()
+        rel = float((a - b).abs().max() / a.abs().max())
+        assert torch.isfinite(b).all()
+        assert rel < (1e-2 if i in (0, 1) else 1e-4), (i, rel)
 
 
 def test_sorted_backward_bf16_grad_value_is_the_rounded_fp32_sum(monkeypatch):

@@ -68,7 +68,9 @@ def _run(grad_sync_factory=None):
                 loss = float(train_step(model, crit, opt, *b, grad_sync=sync))
                 out.append((loss, _grads(model)))
         else:
-            g = TrainStepGraph(model, crit, opt, grad_sync=sync, warmup=2)
+            # text_multiple=1: the eager steps' exact shapes (T = 40); the
+            # 64-token buckets change only rounding (test_text_bucket_*)
+            g = TrainStepGraph(model, crit, opt, grad_sync=sync, warmup=2, text_multiple=1)
             for b in (b1, b2):
                 loss = float(g(*b))
                 out.append((loss, _grads(model)))
@@ -272,7 +274,7 @@ def test_capture_step_applies_the_batch_once():
         model, crit, opt = _model()
         p0 = _params(model)
         if mode == "graph":
-            g = TrainStepGraph(model, crit, opt, warmup=2)
+            g = TrainStepGraph(model, crit, opt, warmup=2, text_multiple=1)
             g(*b)
             assert g.stats()["captures"] == 1 and g.stats()["replays"] == 1
         else:
@@ -357,7 +359,7 @@ def test_failed_capture_falls_back_to_the_eager_step():
                         torch.cuda.synchronize()  # refused during capture
                     return _orig(*a, **k)
                 blk.forward = bad
-                g = TrainStepGraph(model, crit, opt, warmup=1)
+                g = TrainStepGraph(model, crit, opt, warmup=1, text_multiple=1)
                 for b in (b1, b2):
                     out.append((float(g(*b)), _grads(model)))
                 st = g.stats()
@@ -371,3 +373,31 @@ def test_failed_capture_falls_back_to_the_eager_step():
         _check(res)
     finally:
         CKPT[0] = True
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_text_bucket_changes_only_rounding(amp):
+    """Padding the text from T = 40 to the 64-token bucket (pad tokens masked
+    everywhere, models/GroundingDINO/groundingdino.py pad_text) on the HIP
+    path: fp32 losses and gradients equal to 1e-4, bf16 autocast to the
+    north star's bf16 tolerance (1e-2; the GEMM and attention shapes change,
+    so the bf16 roundings do)."""
+    from gdino_amd.stepgraph import TrainStepGraph
+    b = _batch(11, 5)
+    res = {}
+    for mult in (1, 64):
+        model, crit, opt = _model()
+        g = TrainStepGraph(model, crit, opt, amp_dtype=torch.bfloat16 if amp else None, text_multiple=mult)
+        inputs, pf = g._prepare(*b)
+        model.zero_grad(set_to_none=True)
+        loss, d = g._forward_loss(inputs, pf)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[mult] = (inputs["input_ids"].shape[1], float(loss), _grads(model))
+    (t1, l1, g1), (t64, l64, g64) = res[1], res[64]
+    assert (t1, t64) == (40, 64)
+    tol = 1e-2 if amp else 1e-4
+    assert abs(l1 - l64) <= tol * abs(l1), (l1, l64)
+    num = sum(float((g1[n] - g64[n]).norm() ** 2) for n in g1) ** 0.5
+    den = sum(float(g1[n].norm() ** 2) for n in g1) ** 0.5
+    assert num <= tol * den, (num, den)

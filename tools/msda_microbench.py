@@ -163,6 +163,30 @@ def enc_variants(iters, variants=None):
                                   frac=bb / t / PEAK, rel_err_vs_lane32=err)), flush=True)
 
 
+def fwd_gs(iters):
+    """bf16 forward: the geometry-shared kernel (msda_fwd_gs, default) vs the
+    per-lane kernel (GD_MSDA_FWD_GS=0), encoder shape at the init geometry
+    and a 2-px spread, decoder shape; max relative difference between them."""
+    S = sum(h * w for h, w in LEVELS)
+    for lq, geom in ((S, "init"), (S, "spread2"), (900, "uniform")):
+        v, sh, ls, loc, attn, go = inputs(lq, torch.bfloat16)
+        if geom == "init":
+            loc = init_geometry_loc(2)
+        outs = {}
+        for gs in ("0", "1"):
+            os.environ["GD_MSDA_FWD_GS"] = gs
+            fn = lambda: msda.ms_deform_attn_forward(v, sh, ls, loc, attn, 64)  # noqa: E731
+            outs[gs] = fn().float()
+            torch.cuda.synchronize()
+            t = time_it(fn, iters)
+            bf = algo_bytes(2, S, lq, 2)
+            d = float((outs[gs] - outs["0"]).abs().max() / outs["0"].abs().max())
+            print(json.dumps(dict(lq=lq, geom=geom, kernel="msda_fwd_gs" if gs == "1" else "msda_fwd_vec",
+                                  fwd_us=t * 1e6, GBps=bf / t / 1e9, frac=bf / t / PEAK, rel_diff_vs_vec=d)),
+                  flush=True)
+        os.environ.pop("GD_MSDA_FWD_GS", None)
+
+
 def fwd_variants(iters):
     """Forward (bs=2, 800x1333) under each gather batching of msda_fwd_vec
     (GD_MSDA_FWD_SB), encoder shape on the init geometry and a 2-px spread,
@@ -191,6 +215,7 @@ def fwd_variants(iters):
 
 BWD_VARIANTS = [
     ("sorted", {"GD_MSDA_BWD": "sorted"}),
+    ("sorted per-lane-geometry", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_GS": "0"}),
     ("sorted cellsum", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K4": "1"}),
     ("sorted k1-level-by-level", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_K1": "2"}),
     ("sorted one-head-per-wave", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SORTED_HP": "1"}),
@@ -221,13 +246,14 @@ def bwd_variants(iters, only_geom=None, only_variant=None):
         lq = loc.shape[1]
         ref = None
         for name, env in reversed(BWD_VARIANTS):
-            if only_variant and name != only_variant:
+            if only_variant and name not in only_variant.split(","):
                 continue
             saved = {k: os.environ.get(k) for k in ("GD_MSDA_BWD", "GD_MSDA_DETERMINISTIC", "GD_MSDA_SORTED_PROBE",
                                                     "GD_MSDA_SORTED_F", "GD_MSDA_SORTED_K1PIPE",
                                                     "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1",
                                                     "GD_MSDA_SORTED_HP", "GD_MSDA_SWEEP_PF",
-                                                    "GD_MSDA_COUNT_PRIV", "GD_MSDA_SORTED_LL")}
+                                                    "GD_MSDA_COUNT_PRIV", "GD_MSDA_SORTED_LL",
+                                                    "GD_MSDA_SORTED_GS")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
@@ -254,6 +280,7 @@ def bwd_variants(iters, only_geom=None, only_variant=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fwd-variants", action="store_true")
+    ap.add_argument("--fwd-gs", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--enc-variants", action="store_true")
     ap.add_argument("--enc-probes", action="store_true")
@@ -267,6 +294,9 @@ def main():
         return
     if args.fwd_variants:
         fwd_variants(args.iters)
+        return
+    if args.fwd_gs:
+        fwd_gs(args.iters)
         return
     if args.enc_caps:
         enc_variants(args.iters, [ENC_VARIANTS[0], ENC_VARIANTS[1]] + ENC_CAPS)
