@@ -454,15 +454,22 @@ gd_status gd_box_refine_backward(gd_dtype delta_dtype, const float* grad_out, co
 /* ------------------------------------------------------------------------ */
 /*
  * graph: a captured, not yet instantiated hipGraph_t.  Every memset node is
- * replaced by a kernel node (the library's fill kernel, same destination,
+ * replaced by a kernel node (the library's fill kernels, same destination,
  * value and dependencies): on ROCm 7.0 a replayed graph's memset nodes stop
  * taking effect once eager device-to-device copies have run between
  * replays.  Returns the number of nodes replaced, or -1 when a memset node
- * cannot be expressed (element size not 1 / 2 / 4, a pitched 2-D memset,
- * or a byte count not a multiple of 4); the graph is then partly rewritten
- * and must not be used.
+ * cannot be expressed (element size not 1 / 2 / 4, a pitched 2-D memset, a
+ * destination not aligned to its element); all nodes are validated before
+ * any is edited, so on -1 the graph is unchanged.
  */
 int gd_graph_memsets_to_kernels(void* graph);
+/*
+ * stream: a hipStream_t whose capture failed part-way (an operation the
+ * capture refused, e.g. a synchronisation): ends the invalidated capture and
+ * destroys its graph so the stream runs work again.  -> 1 when a capture
+ * was ended, 0 when the stream was not capturing, -1 on a HIP error.
+ */
+int gd_stream_abort_capture(void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Hungarian matching (matcher.py:104-110)                                   */

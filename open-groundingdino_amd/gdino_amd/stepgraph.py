@@ -90,6 +90,7 @@ def _static_like(t: torch.Tensor) -> torch.Tensor:
 
 
 _lib.register("gd_graph_memsets_to_kernels", [ctypes.c_void_p])
+_lib.register("gd_stream_abort_capture", [ctypes.c_void_p])
 
 
 def memsets_to_kernels(graph: "torch.cuda.CUDAGraph") -> int:
@@ -421,17 +422,34 @@ class TrainStepGraph:
             self.optimizer.zero_grad(set_to_none=True)
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
-        c.graph = torch.cuda.CUDAGraph(keep_graph=True)
+        c.graph = g = torch.cuda.CUDAGraph(keep_graph=True)
+        side = self._stream_ctx_stream()
+        torch.cuda.synchronize()
         _log("capture begins")
+        # capture_begin / capture_end by hand instead of torch.cuda.graph:
+        # when the body fails part-way, its __exit__ raises from capture_end
+        # before it restores the current stream, and every later "eager"
+        # launch would go to the invalidated capture stream.  Here the
+        # stream context always unwinds, the invalidated capture is ended
+        # (gd_stream_abort_capture) and the side stream is replaced.
         # thread_local: calls other threads make meanwhile (ProcessGroupNCCL's
         # watchdog polling the events of earlier eager collectives) do not
         # invalidate the capture
-        with torch.cuda.graph(c.graph, pool=self.pool if _SHARED_POOL else None, stream=self._stream_ctx_stream(),
-                              capture_error_mode=_CAPTURE_MODE):
-            loss, loss_dict = self._body(c.inputs, padding_free)
-            c.loss_out.copy_(loss)
-            for k, v in loss_dict.items():
-                c.dict_out[k].copy_(v)
+        with torch.cuda.stream(side):
+            g.capture_begin(pool=self.pool if _SHARED_POOL else None, capture_error_mode=_CAPTURE_MODE)
+            try:
+                loss, loss_dict = self._body(c.inputs, padding_free)
+                c.loss_out.copy_(loss)
+                for k, v in loss_dict.items():
+                    c.dict_out[k].copy_(v)
+            except BaseException:
+                self._abandon_capture(g, side)
+                raise
+            try:
+                g.capture_end()
+            except BaseException:
+                self._abandon_capture(g, side)
+                raise
         torch.cuda.current_stream().wait_stream(self.side)
         if self.grad_sync is None:
             c.grads = [p.grad for p in self.model.parameters() if p.requires_grad]
@@ -439,6 +457,26 @@ class TrainStepGraph:
         c.memsets_replaced = memsets_to_kernels(c.graph)
         c.graph.instantiate()
         _log(f"captured; memset nodes replaced by fill kernels: {c.memsets_replaced}")
+
+    def _abandon_capture(self, g, side):
+        """After a failed capture: end the stream's (invalidated) capture,
+        release the allocator's capture routing, drop the stream."""
+        try:
+            g.capture_end()
+        except BaseException:  # noqa: BLE001 -- the capture is already invalid
+            pass
+        try:
+            fn = _lib.lib().gd_stream_abort_capture
+            fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
+            fn(ctypes.c_void_p(side.cuda_stream))
+        except Exception:  # noqa: BLE001
+            pass
+        try:
+            torch._C._cuda_endAllocateToPool(self.device.index if self.device.index is not None else
+                                             torch.cuda.current_device(), g.pool())
+        except Exception:  # noqa: BLE001 -- already ended by capture_end
+            pass
+        self.side = None
 
     def _stream_ctx_stream(self):
         if self.side is None:

@@ -101,12 +101,6 @@ prof)
   python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
       --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
   ;;
-tune)
-  # TunableOp: tune the step's GEMM shapes, then bench with the table
-  T 900 python3 tools/tune_gemms.py --out tunableop/gdino_train_gfx950.csv > gpurun_out/s_tune.log 2>&1 &&
-  T 600 python3 bench.py --no-cpu-baseline --tunableop tunableop/gdino_train_gfx950.csv \
-      > gpurun_out/s_bench_tunable.log 2>&1
-  ;;
 ab)
   # A/B of every kernel family against its torch composition (GDINO_DISABLE)
   T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_ab_all.log 2>&1 &&
@@ -144,7 +138,7 @@ syncab)
   GDINO_STEPGRAPH_SYNC=event T 600 python3 bench.py --no-cpu-baseline > gpurun_out/s_bench_event.log 2>&1
   ;;
 *)
-  echo "usage: $0 [tests|bench|core|prof|tune|ab|graphs]" >&2
+  echo "usage: $0 [tests|bench|core|prof|ab|graphs|msdapmc|syncab]" >&2
   exit 2
   ;;
 esac

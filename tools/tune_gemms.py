@@ -22,6 +22,13 @@ import torch  # noqa: E402
 
 
 def main():
+    # Round 5: the tuning run faulted the GPU a second time (an illegal
+    # address while TunableOp timed candidate solutions for the encoder's
+    # Linear, profiles/r05e_tunableop_fault.log) after round 4's fix for the
+    # strided BiAttention operands.  Refused unless explicitly forced.
+    if os.environ.get("GDINO_ALLOW_TUNING") != "1":
+        raise SystemExit("tune_gemms.py: TunableOp tuning faulted the GPU twice (rounds 3 and 5); "
+                         "set GDINO_ALLOW_TUNING=1 to run it anyway")
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "tunableop", "gdino_train_gfx950.csv"))
     ap.add_argument("--steps", type=int, default=2)
