@@ -557,6 +557,12 @@ def _run(a, on_gpu, rank, world, local, ctrl):
 
     images = a.bs * world * a.steps
     value = images / elapsed
+    device_check = None
+    if on_gpu:
+        try:  # the MSDA kernels' device-side guards (csrc/msda.hip g_device_err)
+            msda.check_device_status(device)
+        except _lib.GdError as e:
+            device_check = str(e)[:300]
 
     if a.output_dir and not a.forward_only:
         from gdino_amd import checkpoint as ckpt
@@ -616,6 +622,8 @@ def _run(a, on_gpu, rank, world, local, ctrl):
             res["config"]["ckpt_on"] = ckpt_on
         if not math.isfinite(loss_v):
             res["error"] = f"non-finite loss {loss_v}: the step diverged, the throughput is not a valid measurement"
+        if device_check is not None:
+            res["error"] = f"device-side check failed: {device_check}"
         if not a.no_cpu_baseline and world == 1:
             _progress("cpu baseline (host cores)")
             res["cpu_baseline"] = cpu_baseline(a.bs, recompute=a.checkpointing == "on")

@@ -320,6 +320,26 @@ gd_status gd_attn_forward(gd_dtype dtype, int B, int H, int Lq, int Lk, int head
                           const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
                           const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
                           void* out, const int64_t* out_strides, float* lse, gd_stream_t stream);
+/* The same with the dropout seed also read from device memory: the kernels
+ * use seed ^ *seed_dev (seed_dev NULL: seed alone).  A captured HIP graph
+ * bakes a host seed into every replay; a seed tensor the graph refills each
+ * step (a graph-safe torch.randint) gives every replay its own mask, and the
+ * backward reads the same word. */
+gd_status gd_attn_forward_dev(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                              const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                              const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                              const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                              const uint32_t* seed_dev, void* out, const int64_t* out_strides, float* lse,
+                              gd_stream_t stream);
+gd_status gd_attn_backward_dev(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                               const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                               const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                               const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                               const uint32_t* seed_dev, const void* out, const int64_t* out_strides,
+                               const void* grad_out, const int64_t* grad_out_strides, const float* lse,
+                               float* dsum, void* grad_q, const int64_t* grad_q_strides, void* grad_k,
+                               const int64_t* grad_k_strides, void* grad_v, const int64_t* grad_v_strides,
+                               gd_stream_t stream);
 /* dsum: [B, H, Lq] F32 workspace (rowsum(dO . O)); grad_q / grad_k / grad_v
  * are fully written. */
 gd_status gd_attn_backward(gd_dtype dtype, int B, int H, int Lq, int Lk, int head_dim, const void* q,

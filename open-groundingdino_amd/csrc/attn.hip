@@ -54,6 +54,7 @@ gd_status fill(AttnArgs& a, gd_dtype dt, int B, int H, int Lq, int Lk, int hd, c
   a.drop_thresh = uint32_t(fmin(double(dropout_p) * 4294967296.0, 4294967295.0));
   a.drop_scale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
   a.seed = seed;
+  a.seed_dev = nullptr;
   return GD_OK;
 }
 
@@ -95,14 +96,16 @@ using namespace gd;
     if (_s != GD_OK) return _s;      \
   } while (0)
 
-extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
-                                     const int64_t* q_strides, const void* k, const int64_t* k_strides,
-                                     const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
-                                     const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
-                                     void* out, const int64_t* out_strides, float* lse, gd_stream_t stream) {
+extern "C" gd_status gd_attn_forward_dev(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                                         const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                                         const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                                         const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                                         const uint32_t* seed_dev, void* out, const int64_t* out_strides,
+                                         float* lse, gd_stream_t stream) {
   AttnArgs a;
   GD_RET(fill(a, dt, B, H, Lq, Lk, head_dim, q, q_strides, k, k_strides, v, v_strides, mask, mask_kind,
               mask_strides, scale, dropout_p, seed));
+  a.seed_dev = seed_dev;
   if (B == 0) return GD_OK;
   GD_RET(take_strides(a.os, out_strides, out, dt, "out"));
   GD_REQUIRE(lse, "attn: null lse");
@@ -134,11 +137,21 @@ extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, 
   return GD_OK;
 }
 
-extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
-                                      const int64_t* q_strides, const void* k, const int64_t* k_strides,
-                                      const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
-                                      const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
-                                      const void* out,
+extern "C" gd_status gd_attn_forward(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                                     const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                                     const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                                     const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                                     void* out, const int64_t* out_strides, float* lse, gd_stream_t stream) {
+  return gd_attn_forward_dev(dt, B, H, Lq, Lk, head_dim, q, q_strides, k, k_strides, v, v_strides, mask,
+                             mask_kind, mask_strides, scale, dropout_p, seed, nullptr, out, out_strides, lse,
+                             stream);
+}
+
+extern "C" gd_status gd_attn_backward_dev(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                                          const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                                          const void* v, const int64_t* v_strides, const void* mask,
+                                          int mask_kind, const int64_t* mask_strides, float scale, float dropout_p,
+                                          uint32_t seed, const uint32_t* seed_dev, const void* out,
                                       const int64_t* out_strides, const void* grad_out,
                                       const int64_t* grad_out_strides, const float* lse, float* dsum,
                                       void* grad_q, const int64_t* grad_q_strides, void* grad_k,
@@ -147,6 +160,7 @@ extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk,
   AttnArgs a;
   GD_RET(fill(a, dt, B, H, Lq, Lk, head_dim, q, q_strides, k, k_strides, v, v_strides, mask, mask_kind,
               mask_strides, scale, dropout_p, seed));
+  a.seed_dev = seed_dev;
   if (B == 0) return GD_OK;
   GD_RET(take_strides(a.os, out_strides, out, dt, "out"));
   GD_RET(take_strides(a.gs, grad_out_strides, grad_out, dt, "grad_out"));
@@ -187,4 +201,19 @@ extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk,
 #undef GD_AB1
 #undef GD_AB
   return GD_OK;
+}
+
+extern "C" gd_status gd_attn_backward(gd_dtype dt, int B, int H, int Lq, int Lk, int head_dim, const void* q,
+                                      const int64_t* q_strides, const void* k, const int64_t* k_strides,
+                                      const void* v, const int64_t* v_strides, const void* mask, int mask_kind,
+                                      const int64_t* mask_strides, float scale, float dropout_p, uint32_t seed,
+                                      const void* out, const int64_t* out_strides, const void* grad_out,
+                                      const int64_t* grad_out_strides, const float* lse, float* dsum,
+                                      void* grad_q, const int64_t* grad_q_strides, void* grad_k,
+                                      const int64_t* grad_k_strides, void* grad_v, const int64_t* grad_v_strides,
+                                      gd_stream_t stream) {
+  return gd_attn_backward_dev(dt, B, H, Lq, Lk, head_dim, q, q_strides, k, k_strides, v, v_strides, mask,
+                              mask_kind, mask_strides, scale, dropout_p, seed, nullptr, out, out_strides, grad_out,
+                              grad_out_strides, lse, dsum, grad_q, grad_q_strides, grad_k, grad_k_strides, grad_v,
+                              grad_v_strides, stream);
 }

@@ -21,6 +21,9 @@ BERT's and the MHA's output projections read) and returned as the
 with attention-probability dropout (BERT's attention dropout 0.1 in training)
 drawn from a counter-based hash of (seed, b*H+h, q, k) that the backward
 regenerates -- the same distribution as torch's dropout, not its RNG stream.
+The seed is a 1-element device tensor drawn by torch's CUDA generator and
+read by the kernels from memory, so a captured step graph draws a new mask
+per replay (a host seed would be frozen into the graph).
 Anything else uses PyTorch SDPA (ROCm flash / mem-efficient kernels).  CPU
 tensors raise.
 """
@@ -37,6 +40,8 @@ _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _u32 = ctypes.c_uint32
 _lib.register("gd_attn_forward", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u32, _p, _p, _p, _p])
 _lib.register("gd_attn_backward", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u32] + [_p] * 13)
+_lib.register("gd_attn_forward_dev", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u32, _p, _p, _p, _p, _p])
+_lib.register("gd_attn_backward_dev", [_i] * 6 + [_p] * 7 + [_i, _p, _f, _f, _u32, _p] + [_p] * 13)
 
 
 def _st3(t):
@@ -77,7 +82,10 @@ def supported(q, k, v, dropout_p) -> bool:
 
 class AttnFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, mask, scale, dropout_p=0.0, seed=0):
+    def forward(ctx, q, k, v, mask, scale, dropout_p=0.0, seed=None):
+        """seed: None, or a 1-element int32 device tensor -- the dropout mask
+        seed, read by the kernels from device memory (graph-safe: a captured
+        step refills it every replay; the backward reads the same word)."""
         _lib.require_device(q, k, v, mask, what="attention")
         q, k, v = _rows(q), _rows(k), _rows(v)
         b, h, lq, hd = q.shape
@@ -85,18 +93,18 @@ class AttnFunction(torch.autograd.Function):
         m, kind, ms = _mask_args(mask, b, h, lq, lk)
         out = torch.empty(b, lq, h, hd, dtype=q.dtype, device=q.device).transpose(1, 2)
         lse = torch.empty(b, h, lq, dtype=torch.float32, device=q.device)
-        _lib.call("gd_attn_forward", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
-                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), kind, ms, float(scale), float(dropout_p), int(seed),
-                  out.data_ptr(), _st3(out), lse.data_ptr(), _lib.stream_of(q),
+        _lib.call("gd_attn_forward_dev", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
+                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), kind, ms, float(scale), float(dropout_p), 0,
+                  _lib.ptr(seed), out.data_ptr(), _st3(out), lse.data_ptr(), _lib.stream_of(q),
                   flops=4.0 * b * h * lq * lk * hd)  # S = QK^T, O = PV
-        ctx.save_for_backward(q, k, v, m, out, lse)
+        ctx.save_for_backward(q, k, v, m, out, lse, seed)
         ctx.kind, ctx.ms, ctx.scale = kind, tuple(ms) if ms is not None else None, float(scale)
-        ctx.dropout_p, ctx.seed = float(dropout_p), int(seed)
+        ctx.dropout_p = float(dropout_p)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, k, v, m, out, lse = ctx.saved_tensors
+        q, k, v, m, out, lse, seed = ctx.saved_tensors
         b, h, lq, hd = q.shape
         lk = k.shape[2]
         dout = _rows(dout.to(q.dtype))
@@ -104,11 +112,11 @@ class AttnFunction(torch.autograd.Function):
         dsum = torch.empty(b, h, lq, dtype=torch.float32, device=q.device)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         dq, dk, dv = _rows(dq), _rows(dk), _rows(dv)
-        _lib.call("gd_attn_backward", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q), k.data_ptr(),
-                  _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), ctx.kind, ms, ctx.scale, ctx.dropout_p, ctx.seed,
-                  out.data_ptr(), _st3(out), dout.data_ptr(), _st3(dout), lse.data_ptr(), dsum.data_ptr(),
-                  dq.data_ptr(), _st3(dq), dk.data_ptr(), _st3(dk), dv.data_ptr(), _st3(dv), _lib.stream_of(q),
-                  flops=10.0 * b * h * lq * lk * hd)  # S recompute, dP, dV, dQ, dK (2.5x forward)
+        _lib.call("gd_attn_backward_dev", _lib.dtype_code(q), b, h, lq, lk, hd, q.data_ptr(), _st3(q),
+                  k.data_ptr(), _st3(k), v.data_ptr(), _st3(v), _lib.ptr(m), ctx.kind, ms, ctx.scale, ctx.dropout_p,
+                  0, _lib.ptr(seed), out.data_ptr(), _st3(out), dout.data_ptr(), _st3(dout), lse.data_ptr(),
+                  dsum.data_ptr(), dq.data_ptr(), _st3(dq), dk.data_ptr(), _st3(dk), dv.data_ptr(), _st3(dv),
+                  _lib.stream_of(q), flops=10.0 * b * h * lq * lk * hd)  # S recompute, dP, dV, dQ, dK (2.5x fwd)
         return dq, dk, dv, None, None, None, None
 
 
@@ -118,14 +126,10 @@ def attention_hip(q, k, v, attn_mask=None, scale=None, dropout_p=0.0):
         return F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=dropout_p, scale=scale)
     scale = q.shape[-1] ** -0.5 if scale is None else scale
     if dropout_p > 0.0:
-        if q.is_cuda and torch.cuda.is_current_stream_capturing():
-            # a host-drawn seed would be baked into a captured HIP graph and
-            # every replay would apply the same mask: use PyTorch's dropout,
-            # whose Philox offset is graph-safe
-            return F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=dropout_p, scale=scale)
-        # per-call mask seed from torch's (CPU) generator: torch.manual_seed
-        # reproduces it, no device sync
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        # the mask seed drawn on the device by torch's generator (graph-safe:
+        # inside a captured step each replay draws a new one) and read by the
+        # kernels from memory; torch.manual_seed reproduces it
+        seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=q.device)
         return AttnFunction.apply(q, k, v, attn_mask, scale, dropout_p, seed)
     return AttnFunction.apply(q, k, v, attn_mask, scale)
 

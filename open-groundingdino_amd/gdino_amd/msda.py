@@ -28,7 +28,17 @@ from . import _lib
 _p, _i = ctypes.c_void_p, ctypes.c_int
 _lib.register("gd_msda_backward_sorted", [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 +
               [_p, _i, _p, _p, _p, _p, ctypes.c_size_t, _i, _p])
+_lib.register("gd_device_status", [_p])
 GD_MSDA_DETERMINISTIC = 1
+
+
+def check_device_status(device=None) -> None:
+    """Synchronise the current stream and raise GdError when a device-side
+    check of the MSDA kernels fired since the last call (the sorted
+    backward's record-slot guard: a record it refused to store out of
+    bounds).  The check word is cleared by the read."""
+    dev = torch.device(device or "cuda")
+    _lib.call("gd_device_status", torch.cuda.current_stream(dev).cuda_stream)
 
 
 def _workspace_bytes(dt, N, S, M, D, L, Lq, P, hs, flags) -> int:

@@ -425,6 +425,7 @@ class TrainStepGraph:
         c.graph = g = torch.cuda.CUDAGraph(keep_graph=True)
         side = self._stream_ctx_stream()
         torch.cuda.synchronize()
+        self._retire_collectives()
         _log("capture begins")
         # capture_begin / capture_end by hand instead of torch.cuda.graph:
         # when the body fails part-way, its __exit__ raises from capture_end
@@ -457,6 +458,23 @@ class TrainStepGraph:
         c.memsets_replaced = memsets_to_kernels(c.graph)
         c.graph.instantiate()
         _log(f"captured; memset nodes replaced by fill kernels: {c.memsets_replaced}")
+
+    def _retire_collectives(self):
+        """Wait until ProcessGroupNCCL's watchdog has retired every eager
+        collective: once the capture joins the communicator's stream, HIP
+        refuses queries of events last recorded on that stream
+        (hipErrorCapturedEvent), and the watchdog would abort the process
+        polling an earlier work's end event."""
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        groups = [dist.group.WORLD]
+        gs = getattr(self.grad_sync, "group", None)
+        if gs is not None and gs is not dist.group.WORLD:
+            groups.append(gs)
+        for grp in groups:
+            if dist.get_backend(grp) != "nccl":
+                continue
+            grp._wait_for_pending_works()
 
     def _abandon_capture(self, g, side):
         """After a failed capture: end the stream's (invalidated) capture,
@@ -509,6 +527,9 @@ class TrainStepGraph:
         print(f"warning: step graph disabled on rank {self.agree.rank}: {self.fallback_reason}",
               file=sys.stderr, flush=True)
         self.release()
+        # the capture recorded (never ran) the shadow refresh while marking
+        # the shadows current: they still hold a warm-up's weights
+        castcache.clear()
         self.mode = "eager"
 
     # ------------------------------------------------------------- queue

@@ -272,11 +272,7 @@ class GroundingDINO(nn.Module):
         hs, reference, hs_enc, ref_enc, init_box_proposal = self.transformer(
             srcs, masks, None, poss, None, None, text_dict)
 
-        coords = []
-        for ref_sig, box_embed, layer_hs in zip(reference[:-1], self.bbox_embed, hs):
-            coords.append(box_refine(box_embed(layer_hs), ref_sig))  # groundingdino.py:325-327
-        outputs_coord = torch.stack(coords)
-        outputs_class = torch.stack([emb(layer_hs, text_dict) for emb, layer_hs in zip(self.class_embed, hs)])
+        outputs_coord, outputs_class = self._heads_all_layers(hs, reference, text_dict)
         bs, len_td = text_dict["text_token_mask"].shape
         text_mask = torch.zeros(bs, self.max_text_len, dtype=torch.bool, device=images.device)
         text_mask[:, :len_td] = text_dict["text_token_mask"]
@@ -284,6 +280,33 @@ class GroundingDINO(nn.Module):
             interm_class = self.transformer.enc_out_class_embed(hs_enc[-1], text_dict)
             return outputs_class, outputs_coord, text_mask, interm_class, ref_enc[-1], init_box_proposal
         return outputs_class, outputs_coord, text_mask, None, None, None
+
+    def _heads_all_layers(self, hs, reference, text_dict):
+        """The per-layer box and class heads (reference groundingdino.py:
+        325-337): box_refine(bbox_embed[l](hs[l]), reference[l]) and
+        class_embed[l](hs[l], text).  When every layer shares one bbox_embed
+        and one class_embed (dec_pred_bbox_embed_share, the cfg default)
+        the heads run ONCE over all layers' queries, [B, L*Q, C], instead of
+        once per layer: the same per-row arithmetic, one GEMM per MLP layer
+        and one contrastive launch instead of L, and the shared weights'
+        gradients summed inside one weight-gradient GEMM instead of L
+        gradient accumulations.  -> (coords [L, B, Q, 4], logits [L, B, Q, 256])"""
+        L = len(hs)
+        shared = (all(m is self.bbox_embed[0] for m in self.bbox_embed)
+                  and all(m is self.class_embed[0] for m in self.class_embed) and L > 1
+                  and all(h.shape == hs[0].shape for h in hs))
+        if not shared:
+            coords = [box_refine(box_embed(layer_hs), ref_sig)
+                      for ref_sig, box_embed, layer_hs in zip(reference[:-1], self.bbox_embed, hs)]
+            return (torch.stack(coords),
+                    torch.stack([emb(layer_hs, text_dict) for emb, layer_hs in zip(self.class_embed, hs)]))
+        B, Q, C = hs[0].shape
+        x = torch.stack(hs, 1)                                    # [B, L, Q, C]
+        ref = torch.stack(reference[:-1], 1)                      # [B, L, Q, 4]
+        delta = self.bbox_embed[0](x)                             # [B, L, Q, 4]
+        coords = box_refine(delta.reshape(B, L * Q, 4), ref.reshape(B, L * Q, 4)).view(B, L, Q, 4)
+        logits = self.class_embed[0](x.view(B, L * Q, C), text_dict)   # [B, L*Q, 256]
+        return coords.transpose(0, 1), logits.view(B, L, Q, -1).transpose(0, 1)
 
     def forward(self, samples, targets: List = None, **kw):
         captions = kw["captions"] if targets is None else [t["caption"] for t in targets]

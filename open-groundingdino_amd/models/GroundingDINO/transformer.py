@@ -327,7 +327,13 @@ class TransformerDecoder(nn.Module):
             query_sine_embed = gen_sineembed_for_position(ref_input[:, :, 0, :])
             raw_query_pos = self.ref_point_head(query_sine_embed)
             pos_scale = self.query_scale(output) if self.query_scale is not None else 1
-            query_pos = pos_scale * raw_query_pos
+            # (no multiply by the constant 1; and fp32 once per layer: the
+            # layer adds it to the fp32 target three times, with_pos_embed,
+            # and a bf16 + fp32 add takes PyTorch's slow mixed-dtype path --
+            # the values are the ones the promotion would produce)
+            query_pos = raw_query_pos if self.query_scale is None else pos_scale * raw_query_pos
+            if query_pos.dtype != output.dtype and output.dtype == torch.float32:
+                query_pos = query_pos.float()
             output = layer(tgt=output, tgt_query_pos=query_pos, tgt_query_sine_embed=query_sine_embed,
                            tgt_key_padding_mask=tgt_key_padding_mask, tgt_reference_points=ref_input,
                            memory_text=memory_text, text_attention_mask=text_attention_mask, memory=memory,

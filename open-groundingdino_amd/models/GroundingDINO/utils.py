@@ -11,7 +11,7 @@ from torch import Tensor, nn
 
 from gdino_amd.misc import device_const
 
-from gdino_amd import kernels
+from gdino_amd import castcache, kernels
 from gdino_amd.misc import sigmoid_focal_loss  # noqa: F401  (re-export, reference utils.py:152)
 
 
@@ -118,11 +118,11 @@ class MLP(nn.Module):
         self.layers = nn.ModuleList(nn.Linear(a, b) for a, b in zip(dims, outs))
 
     def forward(self, x):
+        # relu(layer(x)) with the ReLU in the GEMM epilogue on the token-linear
+        # route (castcache.linear_relu; elsewhere the plain composition)
         last = self.num_layers - 1
         for i, layer in enumerate(self.layers):
-            x = layer(x)
-            if i < last:
-                x = F.relu(x)
+            x = castcache.linear_relu(x, layer) if i < last else layer(x)
         return x
 
 

@@ -18,7 +18,7 @@ def emulated_product(min_tokens=None):
     from gdino_amd import _lib, wgrad
     emu = emu_lib.lib()
     for name, argtypes in _lib._SIGNATURES.items():
-        if name.startswith("gd_graph_"):  # HIP graph editing: runtime API, not a kernel (no emulator twin)
+        if name.startswith(("gd_graph_", "gd_stream_")):  # HIP graph / capture runtime API: no emulator twin
             continue
         fn = getattr(emu, name)
         fn.argtypes = argtypes

@@ -375,12 +375,59 @@ def test_attention_dropout_matches_reference_with_the_kernel_mask(dtype, tol):
     grad = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(dtype)
     ref.backward(grad.double())
     dev = [t.to(DEV).requires_grad_(True) for t in (q, k, v)]
-    out = AttnFunction.apply(*dev, mask.to(DEV), hd ** -0.5, p, seed)
+    # the seed is read by the kernels from device memory (graph-safe)
+    seed_t = torch.tensor([seed], dtype=torch.int32, device=DEV)
+    out = AttnFunction.apply(*dev, mask.to(DEV), hd ** -0.5, p, seed_t)
     out.backward(grad.to(DEV))
     torch.cuda.synchronize()
     assert _rel(out.cpu(), ref.detach()) < tol
     for name, mine, r in zip(("dq", "dk", "dv"), dev, ref_in):
         assert _rel(mine.grad.cpu(), r.grad) < tol * 3, name
+
+
+def test_attention_dropout_in_a_captured_graph_draws_a_new_mask_per_replay():
+    """BERT's attention dropout inside the captured train step: the mask seed
+    is a device tensor the graph redraws (torch.randint) on every replay, so
+    two replays apply different masks, and each replay's backward uses its
+    own forward's mask (dq / dk / dv consistent with the output: the
+    directional derivative check below)."""
+    from gdino_amd import kernels
+    b, h, lq, lk, hd, p = 2, 12, 256, 256, 64, 0.1
+    q, k, v, mask = _attn_inputs(b, h, lq, lk, hd, "add", torch.bfloat16, seed=7)
+    q, k, v = (t.to(DEV).requires_grad_(True) for t in (q, k, v))
+    mask = mask.to(DEV)
+    g = torch.randn(b, h, lq, hd, device=DEV, dtype=torch.bfloat16)
+
+    def step():
+        for t in (q, k, v):
+            t.grad = None
+        out = kernels.attention(q, k, v, mask, hd ** -0.5, p)
+        out.backward(g)
+        return out
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=side):
+        out = step()
+    outs, grads = [], []
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize()
+        outs.append(out.detach().float().clone())
+        grads.append(v.grad.detach().float().clone())
+    assert float((outs[0] - outs[1]).abs().max()) > 0, "both replays applied the same dropout mask"
+    # dV = P_dropped^T . g: the same mask as the forward (out = P_dropped . V):
+    # <out, dv-direction> identity  sum(g * out) == sum(dv * v)
+    for o, dvv in zip(outs, grads):
+        lhs = float((g.float() * o).sum())
+        rhs = float((dvv * v.detach().float()).sum())
+        scale = float((g.float() * o).abs().sum())
+        assert abs(lhs - rhs) <= 1e-2 * scale, (lhs, rhs, scale)
 
 
 # ------------------------------------------------ contrastive head (HIP)

@@ -93,6 +93,10 @@ benchprof)
   python3 tools/pmc_traffic.py --fetch "$PROF/s_pmc_fetch" --write "$PROF/s_pmc_write" \
       --out gpurun_out/s_pmc_traffic.json > gpurun_out/s_pmc_traffic.log 2>&1
   ;;
+census)
+  # kernel census of the default (checkpointing-off) step graph only
+  prof_trace s_prof --steps 4 --warmup 3 --ckpt-compare off
+  ;;
 prof)
   prof_trace s_prof --steps 3 --warmup 2 &&
   prof_pmc s_pmc_fetch FETCH_SIZE --steps 1 --warmup 1 &&
