@@ -469,6 +469,17 @@ gd_status gd_box_refine_backward(gd_dtype delta_dtype, const float* grad_out, co
                                  int64_t rs0, int64_t rs1, int64_t rs2, int64_t n0, int64_t n1, int64_t n2,
                                  float eps, void* grad_delta, float* grad_ref, gd_stream_t stream);
 
+/* Decoder query anchors of one layer (reference transformer.py:660-672,
+ * utils.py:204-230 gen_sineembed_for_position): ref [nq, bs, 4] fp32 (element
+ * strides rs0..rs2), valid_ratios [bs, L, 4] fp32 contiguous, dim_t [128]
+ * (10000^(2 (j / 2) / 128)) -> ref_input [nq, bs, L, 4] = ref * valid_ratios,
+ * sine [nq, bs, 512] = the (y, x, w, h) sine / cosine embedding of
+ * ref_input[:, :, 0].  Forward only (the anchors carry no gradient).
+ * Python: models/GroundingDINO/utils.query_anchors. */
+gd_status gd_query_anchor_forward(const float* ref, int64_t rs0, int64_t rs1, int64_t rs2, int64_t nq, int64_t bs,
+                                  const float* valid_ratios, int L, const float* dim_t, float* ref_input,
+                                  float* sine, gd_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Captured-graph surgery (the train step as one HIP graph)                  */
 /* ------------------------------------------------------------------------ */

@@ -75,6 +75,39 @@ box_refine_bwd_kernel(const float* __restrict__ grad_out, const float* __restric
   }
 }
 
+
+// Decoder query anchors, per layer (reference transformer.py:660-672 via
+// utils.py:204-230): from the layer's reference boxes ref [nq, bs, 4]
+// (strided) and the valid ratios vr [bs, L, 4]
+//     ref_input[q, b, l, :] = ref[q, b, :] * vr[b, l, :]
+//     sine[q, b, 128 c + j]  = (j even ? sin : cos)(p_c * 2 pi / dim_t[j])
+// with p = ref_input[q, b, 0, :] taken in the order (y, x, w, h) = (1, 0, 2, 3)
+// and dim_t = 10000^(2 (j / 2) / 128) (the caller's device table).  The
+// composition is seven launches per decoder layer (mul, index_select, div,
+// two strided sin / cos, stack, the ratio product); here one, no gradient
+// (the anchors are detached).  One thread per output feature of a (q, b) row.
+__global__ void __launch_bounds__(256)
+query_anchor_kernel(const float* __restrict__ ref, int64_t r0, int64_t r1, int64_t r2, int64_t nq, int64_t bs,
+                    const float* __restrict__ vr, int L, const float* __restrict__ dim_t,
+                    float* __restrict__ ref_input, float* __restrict__ sine) {
+  const int64_t rows = nq * bs;
+  const float two_pi = 6.283185307179586f;  // (float)(2 * math.pi), as the composition's scalar
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < rows * 512; i += int64_t(gridDim.x) * 256) {
+    const int64_t row = i / 512;
+    const int f = int(i - row * 512);
+    const int64_t q = row / bs, b = row - q * bs;
+    const int c = f / 128, j = f - c * 128;
+    const int src = c == 0 ? 1 : (c == 1 ? 0 : c);
+    const float p = ref[q * r0 + b * r1 + src * r2] * vr[b * L * 4 + src];
+    const float v = (p * two_pi) / dim_t[j];
+    sine[i] = (j & 1) ? cosf(v) : sinf(v);
+    if (f < L * 4) {
+      const int l = f / 4, k = f - l * 4;
+      ref_input[row * L * 4 + f] = ref[q * r0 + b * r1 + k * r2] * vr[(b * L + l) * 4 + k];
+    }
+  }
+}
+
 template <typename Fn>
 bool with_delta_type(gd_dtype d, Fn&& fn) {
   if (d == GD_F32) fn(float{});
@@ -134,5 +167,18 @@ extern "C" gd_status gd_box_refine_backward(gd_dtype delta_dtype, const float* g
                        eps, (TD*)grad_delta, grad_ref);
   });
   GD_LAUNCH_CHECK("box_refine_backward");
+  return GD_OK;
+}
+
+extern "C" gd_status gd_query_anchor_forward(const float* ref, int64_t rs0, int64_t rs1, int64_t rs2, int64_t nq,
+                                            int64_t bs, const float* valid_ratios, int L, const float* dim_t,
+                                            float* ref_input, float* sine, gd_stream_t stream) {
+  GD_REQUIRE(nq >= 0 && bs > 0 && L > 0 && L * 4 <= 512, "query_anchor: nq=%lld bs=%lld L=%d", (long long)nq,
+             (long long)bs, L);
+  if (nq == 0) return GD_OK;
+  GD_REQUIRE(ref && valid_ratios && dim_t && ref_input && sine, "query_anchor: null pointer");
+  hipLaunchKernelGGL(query_anchor_kernel, dim3(grid_for(nq * bs * 512)), dim3(256), 0, as_hip(stream), ref, rs0, rs1,
+                     rs2, nq, bs, valid_ratios, L, dim_t, ref_input, sine);
+  GD_LAUNCH_CHECK("query_anchor_forward");
   return GD_OK;
 }

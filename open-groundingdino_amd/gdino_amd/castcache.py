@@ -365,13 +365,16 @@ def _cached_cat(params, dtype):
     else:
         def make():
             return torch.cat(ps).to(dtype)  # = cat of the casts, one cast kernel (and one in backward)
-    if _capturing(ps[0]):
-        return make()
     key = ("cat",) + tuple(id(p) for p in ps)
     vers = tuple(p._version for p in ps) + (_gen(any(p.requires_grad for p in ps)),)
     ent = _cache.get(key)
-    if ent is not None and all(r() is p for r, p in zip(ent[0], ps)) and ent[1] == vers and ent[2] == dtype \
-            and ent[3] == grad:
+    hit = (ent is not None and all(r() is p for r, p in zip(ent[0], ps)) and ent[1] == vers and ent[2] == dtype
+           and ent[3] == grad)
+    if _capturing(ps[0]):
+        # frozen parameters: the eager copy made before the capture (constant
+        # across replays); trainable ones are re-concatenated inside the graph
+        return ent[4] if hit and not any(p.requires_grad for p in ps) else make()
+    if hit:
         return ent[4]
     t = make()
     _cache[key] = (tuple(weakref.ref(p) for p in ps), vers, dtype, grad, t)

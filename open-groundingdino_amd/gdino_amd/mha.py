@@ -17,7 +17,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from . import castcache
-from .misc import split_last
+from .misc import inverted, mask_cache_key, split_last
 
 
 def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor], b: int, h: int,
@@ -25,23 +25,23 @@ def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor],
     """-> bool keep-mask or float additive mask broadcastable to [B, H, Lq, Lk]."""
     if attn_mask is None and key_padding_mask is None:
         return None
-    am = None
-    if attn_mask is not None:
-        am = attn_mask
-        if am.dim() == 2:
-            am = am.view(1, 1, lq, lk)
-        elif am.dim() == 3:
-            am = am.view(b, h, lq, lk)
-    kp = None
-    if key_padding_mask is not None:
-        kp = key_padding_mask.view(b, 1, 1, lk)
-    floats = [m for m in (am, kp) if m is not None and m.dtype != torch.bool]
-    if not floats:
-        keep = None
-        if am is not None:
-            keep = ~am
-        if kp is not None:
-            keep = ~kp if keep is None else keep & ~kp
+    def am_view(m):
+        return m.view(1, 1, lq, lk) if m.dim() == 2 else (m.view(b, h, lq, lk) if m.dim() == 3 else m)
+    am = None if attn_mask is None else am_view(attn_mask)
+    kp = None if key_padding_mask is None else key_padding_mask.view(b, 1, 1, lk)
+    if all(m is None or m.dtype == torch.bool for m in (am, kp)):
+        # bool masks: the inversions and their AND once per mask objects and
+        # step (the layers pass the same masks; misc.inverted caches on them)
+        if am is None:
+            return inverted(key_padding_mask).view(b, 1, 1, lk)
+        if kp is None:
+            return am_view(inverted(attn_mask))
+        key = mask_cache_key(attn_mask, key_padding_mask) + (b, h, lq, lk)
+        c = getattr(attn_mask, "_gd_merged", None)
+        if c is not None and c[0] is key_padding_mask and c[1] == key:
+            return c[2]
+        keep = am_view(inverted(attn_mask)) & inverted(key_padding_mask).view(b, 1, 1, lk)
+        attn_mask._gd_merged = (key_padding_mask, key, keep)
         return keep
     add = torch.zeros((), dtype=dtype, device=(am if am is not None else kp).device)
     for m in (am, kp):

@@ -29,6 +29,34 @@ def device_const(key, make, device) -> Tensor:
     return t
 
 
+# per-tensor derived-mask caches (inverted, mha.merge_masks) are keyed on
+# this epoch too: the step graph bumps it around every capture, so a capture
+# records its own mask kernels instead of baking in a warm-up's result (the
+# static inputs are refilled in place on every replay)
+_MASK_EPOCH = [0]
+
+
+def bump_mask_epoch() -> None:
+    _MASK_EPOCH[0] += 1
+
+
+def mask_cache_key(*ts) -> tuple:
+    return tuple(t._version for t in ts) + (_MASK_EPOCH[0],)
+
+
+def inverted(mask: Tensor) -> Tensor:
+    """~mask, computed once per mask object, version and cache epoch: the
+    layers of one step invert the same text / padding masks again and again
+    (one kernel each)."""
+    key = mask_cache_key(mask)
+    c = getattr(mask, "_gd_inv", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    r = ~mask
+    mask._gd_inv = (key, r)
+    return r
+
+
 def topk_indices(x: Tensor, k: int) -> Tensor:
     """torch.topk(x, k, dim=1)[1] (two-stage proposal selection,
     reference transformer.py:292-296), safe inside a captured HIP graph.
@@ -282,6 +310,8 @@ _lib.register("gd_box_refine_forward", [_i, _p, _i64, _i64, _i64, _p, _i64, _i64
                                         ctypes.c_float, _p, _p])
 _lib.register("gd_box_refine_backward", [_i, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_float, _p,
                                          _p, _p])
+# the decoder's per-layer anchors (models/GroundingDINO/utils.query_anchors)
+_lib.register("gd_query_anchor_forward", [_p] + [_i64] * 5 + [_p, _i] + [_p] * 4)
 _lib.register("gd_add_scaled_forward", [_i, _p, _i, _p, _p, _i64, _i, _i64, _i64, _i, _i, _p, _p])
 _lib.register("gd_add_scaled_backward", [_i, _p, _i, _p, _p, _i64, _i, _i64, _i64, _i, _p, _p, _p, _p])
 

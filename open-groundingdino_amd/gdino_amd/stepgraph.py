@@ -59,7 +59,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib, castcache
-from .misc import local_only, no_padding
+from .misc import bump_mask_epoch, local_only, no_padding
 from .train import BucketedGradSync, weighted_loss
 
 _VERBOSE = os.environ.get("GDINO_STEPGRAPH_VERBOSE") == "1"
@@ -426,6 +426,7 @@ class TrainStepGraph:
         side = self._stream_ctx_stream()
         torch.cuda.synchronize()
         self._retire_collectives()
+        bump_mask_epoch()  # no derived mask computed outside this capture is reused inside it
         _log("capture begins")
         # capture_begin / capture_end by hand instead of torch.cuda.graph:
         # when the body fails part-way, its __exit__ raises from capture_end
@@ -452,6 +453,7 @@ class TrainStepGraph:
                 self._abandon_capture(g, side)
                 raise
         torch.cuda.current_stream().wait_stream(self.side)
+        bump_mask_epoch()  # nor one of the capture's (graph-pool) masks outside it
         if self.grad_sync is None:
             c.grads = [p.grad for p in self.model.parameters() if p.requires_grad]
             self._grads_of = c

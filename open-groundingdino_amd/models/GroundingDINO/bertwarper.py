@@ -72,10 +72,84 @@ class BertModelWarper(nn.Module):
             keep = keep[:, None]
         hidden = self.embeddings(input_ids=input_ids, position_ids=position_ids,
                                  token_type_ids=token_type_ids, inputs_embeds=inputs_embeds)
-        enc = self.encoder(hidden, attention_mask=keep)
-        seq = enc[0] if isinstance(enc, (tuple, list)) else enc.last_hidden_state
+        if self._fast_ok(hidden, head_mask):
+            seq = self._encode_frozen(hidden, keep)
+        else:
+            enc = self.encoder(hidden, attention_mask=keep)
+            seq = enc[0] if isinstance(enc, (tuple, list)) else enc.last_hidden_state
         pooled = self.pooler(seq) if self.pooler is not None else None
         return {"last_hidden_state": seq, "pooler_output": pooled}
+
+    # GDINO_BERT_FAST=0: the transformers layer stack (A/B)
+    FAST = True
+
+    def _fast_ok(self, hidden, head_mask) -> bool:
+        """The frozen-encoder path: every encoder parameter frozen (cfg
+        freeze_keywords ['bert'], train.apply_freeze) or no autograd, bf16
+        autocast on the HIP device, the stock post-norm GELU BERT layout."""
+        import os
+        from gdino_amd import _lib, castcache
+        from gdino_amd.layernorm import WIDTHS
+        cfg = self.config
+        return (self.FAST and os.environ.get("GDINO_BERT_FAST", "1") != "0" and head_mask is None
+                and _lib.on_device(hidden) and castcache.autocast_dtype(hidden) == torch.bfloat16
+                and cfg.hidden_act == "gelu" and not getattr(cfg, "is_decoder", False)
+                and cfg.hidden_size in WIDTHS and cfg.hidden_size % cfg.num_attention_heads == 0
+                and (cfg.hidden_size // cfg.num_attention_heads) in (32, 64)
+                and (not torch.is_grad_enabled() or not any(p.requires_grad for p in self.encoder.parameters())))
+
+    def _encode_frozen(self, hidden, keep):
+        """The 12 BertLayers (transformers modeling_bert BertLayer: self
+        attention, BertSelfOutput, BertIntermediate, BertOutput) on the
+        product's kernels, with nothing to differentiate: Q, K and V as ONE
+        GEMM against the cached concatenated bf16 weight, the masked-attention
+        kernel reading q / k / v in place from it (attention dropout in the
+        kernel), and each ``LayerNorm(dropout(dense(x)) + residual)`` as the
+        add + LayerNorm kernel, whose bf16 twin feeds the next GEMM (no cast
+        kernels).  The same arithmetic as the module stack under bf16
+        autocast (bf16 GEMMs, fp32 residual stream and LayerNorm, bf16 GELU)
+        up to the summation order of the fused Q/K/V product."""
+        import torch.nn.functional as F
+
+        from gdino_amd import castcache
+        from gdino_amd.layernorm import add_norm
+        cfg = self.config
+        dt = torch.bfloat16
+        b, t, c = hidden.shape
+        nh = cfg.num_attention_heads
+        hd = c // nh
+
+        # the Dropout modules' own rates and modes (callers may zero them), as
+        # the module stack reads them
+        def drop(x, m):
+            return F.dropout(x, m.p, m.training)
+
+        def lin(x, layer):
+            return F.linear(x, castcache.cached_cast(layer.weight, dt), castcache.cached_cast(layer.bias, dt))
+
+        def as16(h):
+            tw = getattr(h, "_gd_bf16", None)
+            if tw is not None and tw[1] == h._version and tw[0].shape == h.shape:
+                return tw[0]
+            return h.to(dt)
+
+        with torch.no_grad():
+            h = hidden
+            for layer in self.encoder.layer:
+                sa = layer.attention.self
+                wqkv = castcache._cached_cat([sa.query.weight, sa.key.weight, sa.value.weight], dt)
+                bqkv = castcache._cached_cat([sa.query.bias, sa.key.bias, sa.value.bias], dt)
+                qkv = F.linear(as16(h), wqkv, bqkv)                       # [B, T, 3C]
+                q, k, v = (qkv[..., i * c:(i + 1) * c].view(b, t, nh, hd).transpose(1, 2) for i in range(3))
+                # [B, H, T, hd] over [B, T, H, hd] storage
+                ctx = kernels.attention(q, k, v, keep, hd ** -0.5, sa.dropout.p if sa.dropout.training else 0.0)
+                ctx = ctx.transpose(1, 2).reshape(b, t, c)
+                so = layer.attention.output
+                h = add_norm(so.LayerNorm, h, drop(lin(ctx, so.dense), so.dropout))
+                inter = F.gelu(lin(as16(h), layer.intermediate.dense))
+                out = layer.output
+                h = add_norm(out.LayerNorm, h, drop(lin(inter, out.dense), out.dropout))
+        return h
 
 
 class TextEncoderShell(nn.Module):

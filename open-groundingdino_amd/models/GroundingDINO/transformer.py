@@ -25,13 +25,13 @@ from torch import Tensor, nn
 from gdino_amd import kernels
 from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
-from gdino_amd.misc import box_refine, device_const, no_padding, padding_free, topk_indices
+from gdino_amd.misc import box_refine, device_const, inverted, no_padding, padding_free, topk_indices
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
 from .transformer_vanilla import TransformerEncoderLayer
 from .utils import (MLP, _get_activation_fn, _get_clones, ffn_act, gen_encoder_output_proposals,
-                    gen_sineembed_for_position, get_sine_pos_embed)
+                    get_sine_pos_embed, query_anchors)
 
 _DEBUG_NAN = os.environ.get("GDINO_DEBUG_NAN", "0") == "1"
 # mmcv MSDA wrapper semantics (identity add + dropout) — see ms_deform_attn.py
@@ -155,7 +155,7 @@ class Transformer(nn.Module):
         memory, memory_text = self.encoder(
             src_flatten, pos=lvl_pos_embed_flatten, level_start_index=level_start_index,
             spatial_shapes=spatial_shapes, valid_ratios=valid_ratios, key_padding_mask=mask_flatten,
-            memory_text=text_dict["encoded_text"], text_attention_mask=~text_dict["text_token_mask"],
+            memory_text=text_dict["encoded_text"], text_attention_mask=inverted(text_dict["text_token_mask"]),
             position_ids=text_dict["position_ids"],
             text_self_attention_masks=text_dict["text_self_attention_masks"], shapes_list=shapes_list)
         text_dict["encoded_text"] = memory_text
@@ -206,7 +206,7 @@ class Transformer(nn.Module):
             pos=lvl_pos_embed_flatten.transpose(0, 1), refpoints_unsigmoid=refpoint_embed.transpose(0, 1),
             level_start_index=level_start_index, spatial_shapes=spatial_shapes, valid_ratios=valid_ratios,
             tgt_mask=attn_mask, memory_text=text_dict["encoded_text"],
-            text_attention_mask=~text_dict["text_token_mask"])
+            text_attention_mask=inverted(text_dict["text_token_mask"]))
         if self.two_stage_type == "standard":
             hs_enc = tgt_undetach.unsqueeze(0)
             ref_enc = refpoint_embed_undetach.sigmoid().unsqueeze(0)
@@ -278,7 +278,7 @@ class TransformerEncoder(nn.Module):
                                              attention_mask_l=text_attention_mask)
             if self.text_layers:
                 memory_text = self.text_layers[layer_id](
-                    src=memory_text.transpose(0, 1), src_mask=~text_self_attention_masks,
+                    src=memory_text.transpose(0, 1), src_mask=inverted(text_self_attention_masks),
                     src_key_padding_mask=text_attention_mask,
                     pos=pos_text.transpose(0, 1) if pos_text is not None else None).transpose(0, 1)
             if self.use_transformer_ckpt and train_ckpt:
@@ -323,8 +323,8 @@ class TransformerDecoder(nn.Module):
         ref_points = [reference_points]
         vr = torch.cat([valid_ratios, valid_ratios], -1) if reference_points.shape[-1] == 4 else valid_ratios
         for layer_id, layer in enumerate(self.layers):
-            ref_input = reference_points[:, :, None] * vr[None, :]  # [nq, bs, nlevel, 4]
-            query_sine_embed = gen_sineembed_for_position(ref_input[:, :, 0, :])
+            # ref_input [nq, bs, nlevel, 4], query_sine_embed [nq, bs, 512]
+            ref_input, query_sine_embed = query_anchors(reference_points, vr)
             raw_query_pos = self.ref_point_head(query_sine_embed)
             pos_scale = self.query_scale(output) if self.query_scale is not None else 1
             # (no multiply by the constant 1; and fp32 once per layer: the

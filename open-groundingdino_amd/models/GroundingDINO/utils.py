@@ -11,7 +11,7 @@ from torch import Tensor, nn
 
 from gdino_amd.misc import device_const
 
-from gdino_amd import castcache, kernels
+from gdino_amd import _lib, castcache, kernels
 from gdino_amd.misc import sigmoid_focal_loss  # noqa: F401  (re-export, reference utils.py:152)
 
 
@@ -61,6 +61,29 @@ def gen_sineembed_for_position(pos_tensor: Tensor) -> Tensor:
     coords = (pos_tensor * (2 * math.pi)).index_select(-1, order)
     v = coords[..., None] / dim_t
     return torch.stack((v[..., 0::2].sin(), v[..., 1::2].cos()), dim=-1).flatten(-3)
+
+
+def query_anchors(reference_points: Tensor, vr: Tensor):
+    """One decoder layer's anchors (reference transformer.py:660-672):
+    ref_input = reference_points[:, :, None] * vr[None] ([nq, bs, L, 4]) and
+    gen_sineembed_for_position(ref_input[:, :, 0]) ([nq, bs, 512]).  One HIP
+    kernel (csrc/boxref.hip query_anchor_kernel) for the detached fp32 boxes
+    of the two-stage decoder; the composition otherwise."""
+    if (_lib.enabled("boxrefine") and _lib.on_device(reference_points) and not reference_points.requires_grad
+            and not vr.requires_grad and reference_points.dim() == 3 and reference_points.shape[-1] == 4
+            and reference_points.dtype == torch.float32 and vr.dtype == torch.float32 and vr.dim() == 3
+            and vr.shape[-1] == 4 and vr.shape[0] == reference_points.shape[1]):
+        nq, bs, _ = reference_points.shape
+        L = vr.shape[1]
+        vr = vr.contiguous()
+        ref_input = torch.empty(nq, bs, L, 4, dtype=torch.float32, device=reference_points.device)
+        sine = torch.empty(nq, bs, 512, dtype=torch.float32, device=reference_points.device)
+        _lib.call("gd_query_anchor_forward", reference_points.data_ptr(), *reference_points.stride(), nq, bs,
+                  vr.data_ptr(), L, _dim_t(128, 10000, vr.device).data_ptr(), ref_input.data_ptr(),
+                  sine.data_ptr(), _lib.stream_of(vr))
+        return ref_input, sine
+    ref_input = reference_points[:, :, None] * vr[None, :]
+    return ref_input, gen_sineembed_for_position(ref_input[:, :, 0, :])
 
 
 def gen_encoder_output_proposals(memory: Tensor, memory_padding_mask: Tensor, spatial_shapes: Tensor,

@@ -961,3 +961,32 @@ def test_emulated_geometry_shared_kernels_match_per_lane_kernels(local, outliers
         assert torch.isfinite(b).all(), name
         assert E.rel_err(b.double().numpy(), a.double().numpy()) < (1e-2 if name in ("out", "grad_value") else 1e-5), \
             (name, E.rel_err(b.double().numpy(), a.double().numpy()))
+
+
+@pytest.mark.parametrize("transposed", [False, True])
+def test_emulated_query_anchors(transposed, monkeypatch):
+    """One decoder layer's anchors (ref_input = ref * valid_ratios and the
+    (y, x, w, h) sine embedding of its level-0 slice) from the fused kernel
+    (csrc/boxref.hip query_anchor_kernel) vs the composition
+    (gen_sineembed_for_position; GDINO_DISABLE=boxrefine): ref_input
+    bitwise (the same fp32 products), the embedding to the sin / cos
+    implementations' ulps."""
+    from emu_product import emulated_product
+    from models.GroundingDINO.utils import query_anchors
+    g = torch.Generator().manual_seed(3)
+    ref = torch.rand(2, 37, 4, generator=g)
+    ref = ref.transpose(0, 1) if transposed else ref.transpose(0, 1).contiguous()  # [nq, bs, 4]
+    vr = torch.cat([torch.rand(2, 4, 2, generator=g) * 0.5 + 0.5] * 2, -1)          # [bs, L, 4]
+
+    def run(disable):
+        if disable:
+            monkeypatch.setenv("GDINO_DISABLE", "boxrefine")
+        else:
+            monkeypatch.delenv("GDINO_DISABLE", raising=False)
+        with emulated_product():
+            return query_anchors(ref, vr)
+
+    (ri, se), (ri0, se0) = run(False), run(True)
+    assert ri.shape == ri0.shape == (37, 2, 4, 4) and se.shape == se0.shape == (37, 2, 512)
+    assert torch.equal(ri, ri0)
+    assert float((se - se0).abs().max()) < 2e-6

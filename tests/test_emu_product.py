@@ -210,3 +210,47 @@ def test_bi_attention_token_major_core_on_the_emulated_kernels():
     assert _rel(ov, rv) < 1e-5 and _rel(ol, rl) < 1e-5
     for a, r in zip(mine, ref):
         assert _rel(a.grad, r.grad) < 1e-5
+
+
+def test_frozen_bert_fast_encoder_matches_the_layer_stack():
+    """BertModelWarper._encode_frozen (fused Q/K/V GEMM, in-place q / k / v
+    reads by the attention kernel, add + LayerNorm kernel with its bf16 twin
+    feeding the next GEMM) against transformers' BertLayer stack on the same
+    emulated kernels, bf16 autocast, train mode with the Dropout modules'
+    rates zeroed (the fast path reads the modules, not the config, as the
+    GPU parity tests zero them): one layer agrees to bf16 GEMM
+    rounding flips (the fused Q/K/V product sums in another order); twelve
+    random-init layers amplify those flips, still well inside the north
+    star's bf16 1e-2.  Nothing is recorded for autograd (frozen encoder)."""
+    from gdino_amd.config import make_args
+    from gdino_amd.train import build_training
+    from models.GroundingDINO.bertwarper import BertModelWarper
+    torch.manual_seed(0)
+    model, _, _, _ = build_training(make_args(device="cpu", enc_layers=1, dec_layers=1, num_queries=100),
+                                    torch.device("cpu"))
+    bert = model.bert
+    bert.train()
+    for m in bert.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    assert not any(p.requires_grad for p in bert.encoder.parameters())
+    ids = torch.randint(1000, 2000, (2, 40))
+    kw = dict(input_ids=ids, attention_mask=torch.ones(2, 40, 40, dtype=torch.bool),
+              token_type_ids=torch.zeros_like(ids), position_ids=torch.arange(40)[None].repeat(2, 1))
+    layers = bert.encoder.layer
+
+    def run(fast, n):
+        bert.encoder.layer = layers[:n]
+        saved = BertModelWarper.FAST
+        BertModelWarper.FAST = fast
+        try:
+            with emu_product.emulated_product(), torch.autocast("cpu", dtype=torch.bfloat16):
+                return bert(**kw)["last_hidden_state"]
+        finally:
+            BertModelWarper.FAST = saved
+            bert.encoder.layer = layers
+    for n, tol in ((1, 2e-4), (12, 1e-2)):
+        ref, fast = run(False, n), run(True, n)
+        assert fast.grad_fn is None and fast.dtype == ref.dtype == torch.float32
+        rel = float((fast - ref).norm() / ref.norm())
+        assert rel < tol, (n, rel)

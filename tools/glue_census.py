@@ -28,6 +28,9 @@ SKIP = ("mm", "addmm", "bmm", "_addmm_activation", "baddbmm", "view", "_unsafe_v
         "new_empty_strided", "_to_copy_noop", "lift_fresh", "_reshape_alias", "set_", "record_stream")
 
 
+GEMMS = ("mm", "addmm", "bmm", "_addmm_activation", "baddbmm")
+
+
 def _site():
     node = torch._C._current_autograd_node()
     if node is not None:
@@ -39,16 +42,17 @@ def _site():
 
 
 class Census(TorchDispatchMode):
-    def __init__(self, min_numel):
+    def __init__(self, min_numel, gemms=False):
         super().__init__()
         self.min_numel = min_numel
+        self.gemms = gemms
         self.count = collections.Counter()
         self.bytes = collections.Counter()
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
         name = func.overloadpacket.__name__
-        if name in SKIP:
+        if name in SKIP and not (self.gemms and name in GEMMS):
             return out
         ts = [a for a in args if isinstance(a, torch.Tensor)]
         outs = out if isinstance(out, (tuple, list)) else (out,)
@@ -69,6 +73,8 @@ def main():
     ap.add_argument("--min-numel", type=int, default=1_000_000)
     ap.add_argument("--out", default="gpurun_out/glue.txt")
     ap.add_argument("--checkpointing", choices=("on", "off"), default="off")
+    ap.add_argument("--gemms", action="store_true", help="also count the library GEMM ops")
+    ap.add_argument("--by-count", type=int, default=0, help="also list the N most frequent op sites")
     a = ap.parse_args()
     from gdino_amd.config import make_args
     from gdino_amd.train import build_training, set_activation_checkpointing, synthetic_batch, train_step
@@ -81,7 +87,7 @@ def main():
     for _ in range(2):
         train_step(model, crit, opt, *b)
     torch.cuda.synchronize()
-    c = Census(a.min_numel)
+    c = Census(a.min_numel, a.gemms)
     with c:
         train_step(model, crit, opt, *b)
     torch.cuda.synchronize()
@@ -92,6 +98,13 @@ def main():
                 % (a.min_numel, sum(c.count.values()), tot / 1e9))
         for k, v in c.bytes.most_common():
             f.write("%7.1f MB n=%3d  %-22s %-60s %s\n" % (v / 1e6, c.count[k], k[0], k[2][:60], k[1][:140]))
+        if a.by_count:
+            by_site = collections.Counter()
+            for k, n in c.count.items():
+                by_site[(k[0], k[2])] += n
+            f.write("\n--- the %d most frequent (op, site) pairs, all shapes\n" % a.by_count)
+            for (op, site), n in by_site.most_common(a.by_count):
+                f.write("n=%4d  %-26s %s\n" % (n, op, site[:90]))
     print(open(a.out).read()[:6000])
 
 

@@ -25,6 +25,7 @@ prof_trace() {  # name, bench args...
   local kt; kt=$(find "$PROF/$name" -name '*kernel_trace.csv' | head -n 1 || true)
   if [ -n "$kt" ]; then
     python3 tools/trace_steps.py --skip 2 "$kt" > "gpurun_out/$name/steady_state.txt" 2>&1 || true
+    if [ "${KEEP_TRACE:-0}" = 1 ]; then gzip -c "$kt" > "gpurun_out/$name/kernel_trace.csv.gz"; fi
   fi
 }
 # one PMC pass (one counter group per run)
