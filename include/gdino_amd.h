@@ -423,6 +423,27 @@ gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_
                                     float* grad_weight, float* grad_bias, void* workspace,
                                     gd_stream_t stream);
 
+/* Three-input add + LayerNorm of the deformable layers' attention sublayer,
+ * C = 256: y = LayerNorm(x + (r + dropout(r2))) -- x the fp32 residual
+ * stream, r the fp32 identity the MSDA module adds and r2 its bf16 output
+ * (reference ms_deform_attn.py `self.dropout(output) + identity`, then
+ * transformer.py:789-808 `norm1(src + dropout1(src2))` with dropout1 = 0).
+ * Dropout keeps (row, col) by a counter-based hash of seed ^ *seed_dev
+ * (seed_dev NULL: seed alone), kept values bf16(v / (1 - p)); the backward
+ * regenerates the mask.  Backward: grad_x = the gradient of x and of r (the
+ * same values), grad_r2 (bf16, optional) = bf16(bf16(ds) / (1 - p)) where
+ * kept; grad_weight / grad_bias fp32 (workspace:
+ * gd_add_layernorm_workspace_bytes(256)).  Python: gdino_amd.layernorm.add_norm3. */
+gd_status gd_add_layernorm3_forward(const float* x, const float* r, const void* r2_bf16, const float* weight,
+                                    const float* bias, int64_t rows, int C, float eps, float drop_p, uint32_t seed,
+                                    const uint32_t* seed_dev, float* y, void* y_bf16, float* mean, float* rstd,
+                                    gd_stream_t stream);
+gd_status gd_add_layernorm3_backward(const float* x, const float* r, const void* r2_bf16, const float* weight,
+                                     const float* grad_y, const float* mean, const float* rstd, int64_t rows, int C,
+                                     float drop_p, uint32_t seed, const uint32_t* seed_dev, float* grad_x,
+                                     void* grad_r2_bf16, float* grad_weight, float* grad_bias, void* workspace,
+                                     gd_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Scaled residual ending (fuse_modules.py:285-286, swin_transformer.py:295-296) */
 /* ------------------------------------------------------------------------ */

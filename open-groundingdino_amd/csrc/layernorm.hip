@@ -200,6 +200,158 @@ addln_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Three-input variant for the deformable layers' attention sublayer (C = 256):
+//   y = LayerNorm(x + (r + drop(r2)))
+// x the fp32 residual stream, r the fp32 identity the MSDA module adds
+// (reference ms_deform_attn.py `self.dropout(output) + identity`), r2 its
+// bf16 output projection, drop() the module's dropout: the reference's
+// bf16 dropout kernel, mixed bf16 + fp32 add and fp32 add + LayerNorm in one
+// pass.  Dropout keeps element (row, col) when a counter-based hash of the
+// seed (host value XOR the device word, graph-safe) clears p * 2^32; kept
+// values are rounded to bf16 after the 1 / (1 - p) scale, as the reference's
+// bf16 dropout output is.  The backward regenerates the mask: dx = dr = ds,
+// dr2 = bf16(bf16(ds) * scale) where kept (autograd's cast of the gradient
+// to the bf16 branch, then the dropout backward).
+__device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t row, uint32_t col) {
+  uint32_t h = (col * 0x9E3779B1u) ^ (row * 0x85EBCA77u) ^ seed;
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+
+struct Drop3 {
+  float scale;        // 1 / (1 - p)
+  uint32_t thresh;    // drop when hash < thresh (p * 2^32)
+  uint32_t seed;
+  const uint32_t* seed_dev;  // or NULL
+};
+
+template <bool DROP>
+__device__ __forceinline__ float branch3(const uint16_t* r2, int64_t o, uint32_t row, int col, const Drop3& d) {
+  const float v = bf16_to_f32(r2[o]);
+  if constexpr (!DROP) {
+    return v;
+  } else {
+    return drop_hash(d.seed, row, uint32_t(col)) >= d.thresh ? bf16_to_f32(f32_to_bf16(v * d.scale)) : 0.f;
+  }
+}
+
+template <int C, bool DROP>
+__global__ void __launch_bounds__(256)
+addln3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ r, const uint16_t* __restrict__ r2,
+                  const float* __restrict__ w, const float* __restrict__ b, int64_t rows, float eps, Drop3 d,
+                  float* __restrict__ y, uint16_t* __restrict__ y16, float* __restrict__ mean_out,
+                  float* __restrict__ rstd_out) {
+  constexpr int E = C / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  if (DROP && d.seed_dev) d.seed ^= *d.seed_dev;
+  float wv[E], bv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    wv[e] = w[lane + 64 * e];
+    bv[e] = b[lane + 64 * e];
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    float s[E];
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      s[e] = x[o] + (branch3<DROP>(r2, o, uint32_t(row), lane + 64 * e, d) + r[o]);
+      sum += s[e];
+    }
+    const float mean = wsum(sum) / float(C);
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) sq += (s[e] - mean) * (s[e] - mean);
+    const float rstd = rsqrtf(wsum(sq) / float(C) + eps);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float v = (s[e] - mean) * rstd * wv[e] + bv[e];
+      y[row * C + lane + 64 * e] = v;
+      if (y16) y16[row * C + lane + 64 * e] = f32_to_bf16(v);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <int C, bool DROP>
+__global__ void __launch_bounds__(256)
+addln3_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ r,
+                  const uint16_t* __restrict__ r2, const float* __restrict__ w, const float* __restrict__ mean_in,
+                  const float* __restrict__ rstd_in, int64_t rows, Drop3 d, float* __restrict__ dx,
+                  uint16_t* __restrict__ dr2, float* __restrict__ part_w, float* __restrict__ part_b) {
+  constexpr int E = C / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  if (DROP && d.seed_dev) d.seed ^= *d.seed_dev;
+  float wv[E], gw[E], gb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    wv[e] = w[lane + 64 * e];
+    gw[e] = gb[e] = 0.f;
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[E], g[E];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      const float s = x[o] + (branch3<DROP>(r2, o, uint32_t(row), lane + 64 * e, d) + r[o]);
+      xh[e] = (s - mean) * rstd;
+      const float dv = dy[o];
+      gw[e] += dv * xh[e];
+      gb[e] += dv;
+      g[e] = dv * wv[e];
+      sg += g[e];
+      sgx += g[e] * xh[e];
+    }
+    const float mg = wsum(sg) / float(C), mgx = wsum(sgx) / float(C);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      const float ds = rstd * (g[e] - mg - xh[e] * mgx);
+      dx[o] = ds;
+      if (dr2) {
+        float v = bf16_to_f32(f32_to_bf16(ds));
+        if (DROP) v = drop_hash(d.seed, uint32_t(row), uint32_t(lane + 64 * e)) >= d.thresh ? v * d.scale : 0.f;
+        dr2[o] = f32_to_bf16(v);
+      }
+    }
+  }
+  __shared__ float red[2][4][C];
+  const int wv_i = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    red[0][wv_i][lane + 64 * e] = gw[e];
+    red[1][wv_i][lane + 64 * e] = gb[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part_w[int64_t(blockIdx.x) * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    part_b[int64_t(blockIdx.x) * C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+Drop3 make_drop3(float p, uint32_t seed, const uint32_t* seed_dev) {
+  Drop3 d;
+  d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const double t = double(p) * 4294967296.0;
+  d.thresh = p > 0.f ? uint32_t(t >= 4294967295.0 ? 4294967295.0 : t) : 0u;
+  d.seed = seed;
+  d.seed_dev = seed_dev;
+  return d;
+}
+
 constexpr int kLnBlocks = 512;  // backward grid: 2048 waves, one partial row per block
 
 template <typename Fn>
@@ -303,5 +455,62 @@ extern "C" gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, 
                        kLnBlocks, C, grad_weight, grad_bias);
     GD_LAUNCH_CHECK("add_layernorm_reduce");
   }
+  return GD_OK;
+}
+
+extern "C" gd_status gd_add_layernorm3_forward(const float* x, const float* r, const void* r2_bf16,
+                                              const float* weight, const float* bias, int64_t rows, int C,
+                                              float eps, float drop_p, uint32_t seed, const uint32_t* seed_dev,
+                                              float* y, void* y_bf16, float* mean, float* rstd,
+                                              gd_stream_t stream) {
+  GD_REQUIRE(rows >= 0 && C == 256, "add_layernorm3: rows=%lld C=%d (C = 256)", (long long)rows, C);
+  GD_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "add_layernorm3: dropout p=%f", double(drop_p));
+  if (rows == 0) return GD_OK;
+  GD_REQUIRE(x && r && r2_bf16 && weight && bias && y && mean && rstd, "add_layernorm3_forward: null pointer");
+  const int64_t blocks64 = (rows + 3) / 4;
+  const unsigned blocks = unsigned(blocks64 < 8192 ? blocks64 : 8192);
+  const Drop3 d = make_drop3(drop_p, seed, seed_dev);
+  if (drop_p > 0.f)
+    hipLaunchKernelGGL((addln3_fwd_kernel<256, true>), dim3(blocks), dim3(256), 0, as_hip(stream), x, r,
+                       (const uint16_t*)r2_bf16, weight, bias, rows, eps, d, y, (uint16_t*)y_bf16, mean, rstd);
+  else
+    hipLaunchKernelGGL((addln3_fwd_kernel<256, false>), dim3(blocks), dim3(256), 0, as_hip(stream), x, r,
+                       (const uint16_t*)r2_bf16, weight, bias, rows, eps, d, y, (uint16_t*)y_bf16, mean, rstd);
+  GD_LAUNCH_CHECK("add_layernorm3_fwd");
+  return GD_OK;
+}
+
+extern "C" gd_status gd_add_layernorm3_backward(const float* x, const float* r, const void* r2_bf16,
+                                               const float* weight, const float* grad_y, const float* mean,
+                                               const float* rstd, int64_t rows, int C, float drop_p, uint32_t seed,
+                                               const uint32_t* seed_dev, float* grad_x, void* grad_r2_bf16,
+                                               float* grad_weight, float* grad_bias, void* workspace,
+                                               gd_stream_t stream) {
+  GD_REQUIRE(rows >= 0 && C == 256, "add_layernorm3: rows=%lld C=%d (C = 256)", (long long)rows, C);
+  GD_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "add_layernorm3: dropout p=%f", double(drop_p));
+  GD_REQUIRE(grad_weight && grad_bias && workspace, "add_layernorm3_backward: grad_weight / grad_bias / workspace");
+  hipStream_t s = as_hip(stream);
+  if (rows == 0) {
+    GD_HIP_CHECK(fill_u32_async(grad_weight, 0u, sizeof(float) * C, s));
+    GD_HIP_CHECK(fill_u32_async(grad_bias, 0u, sizeof(float) * C, s));
+    return GD_OK;
+  }
+  GD_REQUIRE(x && r && r2_bf16 && weight && grad_y && mean && rstd && grad_x,
+             "add_layernorm3_backward: null pointer");
+  float* part_w = static_cast<float*>(workspace);
+  float* part_b = part_w + int64_t(kLnBlocks) * C;
+  const Drop3 d = make_drop3(drop_p, seed, seed_dev);
+  if (drop_p > 0.f)
+    hipLaunchKernelGGL((addln3_bwd_kernel<256, true>), dim3(kLnBlocks), dim3(256), 0, s, grad_y, x, r,
+                       (const uint16_t*)r2_bf16, weight, mean, rstd, rows, d, grad_x, (uint16_t*)grad_r2_bf16,
+                       part_w, part_b);
+  else
+    hipLaunchKernelGGL((addln3_bwd_kernel<256, false>), dim3(kLnBlocks), dim3(256), 0, s, grad_y, x, r,
+                       (const uint16_t*)r2_bf16, weight, mean, rstd, rows, d, grad_x, (uint16_t*)grad_r2_bf16,
+                       part_w, part_b);
+  GD_LAUNCH_CHECK("add_layernorm3_bwd");
+  hipLaunchKernelGGL(addln_reduce_kernel, dim3(unsigned((C + 15) / 16)), dim3(1024), 0, s, part_w, part_b, kLnBlocks,
+                     C, grad_weight, grad_bias);
+  GD_LAUNCH_CHECK("add_layernorm3_reduce");
   return GD_OK;
 }

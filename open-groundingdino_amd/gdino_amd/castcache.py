@@ -292,6 +292,17 @@ def _token_linear_ok(x, params, out_features, dt):
     return "lib" if wgrad.lib_eligible(x, dt) else None
 
 
+def linear2d(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
+    """F.linear(x, w, b) as ONE 2-D GEMM over the flattened tokens: F.linear
+    on a 3-D input that cannot be viewed 2-D (a [L, B, C] transpose)
+    dispatches a bmm against the weight expanded to [L, C_out, C_in]; here
+    such an input is copied contiguous first (reshape)."""
+    if x.dim() <= 2 or x.is_contiguous():
+        return F.linear(x, w, b)
+    x2 = x.reshape(-1, x.shape[-1])
+    return F.linear(x2, w, b).view(*x.shape[:-1], w.shape[0])
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     """F.linear with cached weight / bias casts under autocast."""
     dt = autocast_dtype(x) if ENABLED else None
@@ -303,8 +314,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
         if route is not None:
             from . import wgrad
             return wgrad.token_linear(x, wc, bc, [weight], [] if bias is None else [bias], route == "lib")
-        return F.linear(x, wc, bc)
-    return F.linear(x, weight, bias)
+        return linear2d(x, wc, bc)
+    return linear2d(x, weight, bias)
 
 
 # GDINO_FUSED_RELU=0: the activation as its own kernel (A/B)
@@ -419,5 +430,5 @@ def linear_shared_input(x: torch.Tensor, layers):
         from . import wgrad
         y = wgrad.token_linear(x, w, b, [m.weight for m in layers], [m.bias for m in layers], route == "lib")
     else:
-        y = F.linear(x, w, b)
+        y = linear2d(x, w, b)
     return list(split_last(y, [m.out_features for m in layers]))

@@ -97,6 +97,74 @@ class AddLayerNormFunction(torch.autograd.Function):
                 db if ctx.needs_input_grad[3] else None, None, None)
 
 
+_u32 = ctypes.c_uint32
+_lib.register("gd_add_layernorm3_forward", [_p, _p, _p, _p, _p, _i64, _i, _f, _f, _u32, _p, _p, _p, _p, _p, _p])
+_lib.register("gd_add_layernorm3_backward", [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _u32, _p, _p, _p, _p, _p,
+                                              _p, _p])
+
+
+class AddLayerNorm3Function(torch.autograd.Function):
+    """y = LayerNorm(x + (r + dropout_p(r2))): x, r fp32, r2 bf16, C = 256
+    (csrc/layernorm.hip addln3_*).  seed: None (p = 0) or a 1-element int32
+    device tensor the kernels read (a captured step draws a new mask per
+    replay); the backward regenerates the mask from it."""
+
+    @staticmethod
+    def forward(ctx, x, r, r2, weight, bias, eps, p, seed, twin=True):
+        rows = x.numel() // 256
+        y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        y16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if _bf16_twin_wanted(x, twin) else None
+        _lib.call("gd_add_layernorm3_forward", x.data_ptr(), r.data_ptr(), r2.data_ptr(), weight.data_ptr(),
+                  bias.data_ptr(), rows, 256, float(eps), float(p), 0, _lib.ptr(seed), y.data_ptr(), _lib.ptr(y16),
+                  mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(x),
+                  nbytes=rows * (256 * (4 + 4 + 2 + 4 + (0 if y16 is None else 2)) + 8))
+        if y16 is not None:
+            y._gd_bf16 = (y16, y._version)
+        ctx.save_for_backward(x, r, r2, weight, mean, rstd, seed)
+        ctx.p = float(p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, r, r2, weight, mean, rstd, seed = ctx.saved_tensors
+        rows = x.numel() // 256
+        dy = dy.float().contiguous()
+        dx = torch.empty_like(x)
+        dr2 = torch.empty_like(r2) if ctx.needs_input_grad[2] else None
+        dw = torch.empty(256, dtype=torch.float32, device=x.device)
+        db = torch.empty(256, dtype=torch.float32, device=x.device)
+        ws = _workspace(256, x.device)
+        _lib.call("gd_add_layernorm3_backward", x.data_ptr(), r.data_ptr(), r2.data_ptr(), weight.data_ptr(),
+                  dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, 256, ctx.p, 0, _lib.ptr(seed),
+                  dx.data_ptr(), _lib.ptr(dr2), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), _lib.stream_of(x),
+                  nbytes=rows * (256 * (4 + 4 + 4 + 2 + 4 + (2 if dr2 is not None else 0)) + 8))
+        # x and r receive the same gradient (one tensor: autograd never
+        # accumulates into a gradient it does not own alone)
+        return (dx if ctx.needs_input_grad[0] else None, dx if ctx.needs_input_grad[1] else None, dr2,
+                dw if ctx.needs_input_grad[3] else None, db if ctx.needs_input_grad[4] else None, None, None, None,
+                None)
+
+
+def add_norm3(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, r2: torch.Tensor, dropout: nn.Module,
+              bf16_twin: bool = True) -> torch.Tensor:
+    """norm(x + (r + dropout(r2))): the deformable layers' attention sublayer
+    with the MSDA module's identity add and output dropout folded in (one
+    kernel each way instead of dropout, a mixed bf16 + fp32 add and
+    add + LayerNorm).  x, r fp32 [..., 256], r2 bf16 of the same shape,
+    ``dropout`` an nn.Dropout (its rate and mode) or nn.Identity; None when
+    not applicable (the caller runs the composition)."""
+    p = float(getattr(dropout, "p", 0.0)) if dropout.training else 0.0
+    if not (supported(norm, x, r) and x.shape[-1] == 256 and x.dtype == r.dtype == torch.float32
+            and r2.dtype == torch.bfloat16 and r2.shape == x.shape and (p == 0.0 or isinstance(dropout, nn.Dropout))
+            and 0.0 <= p < 1.0):
+        return None
+    seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=x.device) if p > 0 else None
+    return AddLayerNorm3Function.apply(x.contiguous(), r.contiguous(), r2.contiguous(), norm.weight, norm.bias,
+                                       norm.eps, p, seed, bool(bf16_twin))
+
+
 def layer_norm(norm: nn.LayerNorm, x: torch.Tensor, bf16_twin: bool = True) -> torch.Tensor:
     """norm(x) with no residual (Swin's pre-norms and patch-merging norm,
     swin_transformer.py:245, 296, 357): the same kernels with a NULL residual,

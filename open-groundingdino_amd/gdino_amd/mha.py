@@ -67,7 +67,7 @@ class _PackedInProj(torch.autograd.Function):
     def forward(ctx, w, b, xa, xb, split):
         ctx.save_for_backward(w, xa, xb)
         ctx.split = split
-        return F.linear(xa, w[:split], b[:split]), F.linear(xb, w[split:], b[split:])
+        return castcache.linear2d(xa, w[:split], b[:split]), castcache.linear2d(xb, w[split:], b[split:])
 
     @staticmethod
     def backward(ctx, dya, dyb):
@@ -140,7 +140,7 @@ class MultiheadAttention(nn.Module):
                 return ya, k, v
 
         def lin(x, r0, r1):
-            return F.linear(x, w[r0:r1], None if bias is None else bias[r0:r1])
+            return castcache.linear2d(x, w[r0:r1], None if bias is None else bias[r0:r1])
 
         if query is key:
             q, k = split_last(lin(query, 0, 2 * e), (e, e))

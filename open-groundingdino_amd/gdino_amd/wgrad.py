@@ -180,7 +180,12 @@ class TokenLinear(torch.autograd.Function):
             y = y.view(*xc.shape[:-1], wc.shape[0])
             ctx.save_for_backward(xc, wc, y)
         else:
-            y = F.linear(xc, wc, bc)
+            # one 2-D GEMM over the flattened tokens: F.linear on a 3-D input
+            # that cannot be viewed 2-D (the decoder's [nq, bs, C] transposes)
+            # dispatches a bmm against the weight expanded to [nq, C, C]
+            x2 = xc.reshape(-1, xc.shape[-1])
+            y2 = torch.mm(x2, wc.t()) if bc is None else torch.addmm(bc, x2, wc.t())
+            y = y2.view(*xc.shape[:-1], wc.shape[0])
             ctx.save_for_backward(xc, wc)
         ctx.relu = relu
         ctx.lib_wgrad = lib_wgrad

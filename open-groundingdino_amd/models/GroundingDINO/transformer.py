@@ -23,12 +23,13 @@ import torch.utils.checkpoint as checkpoint
 from torch import Tensor, nn
 
 from gdino_amd import kernels
-from gdino_amd.layernorm import add_norm
+from gdino_amd.layernorm import add_norm, add_norm3
 from gdino_amd.mha import MultiheadAttention
 from gdino_amd.misc import box_refine, device_const, inverted, no_padding, padding_free, topk_indices
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
+from .ms_deform_attn import msda_attend
 from .transformer_vanilla import TransformerEncoderLayer
 from .utils import (MLP, _get_activation_fn, _get_clones, ffn_act, gen_encoder_output_proposals,
                     get_sine_pos_embed, query_anchors)
@@ -44,6 +45,11 @@ def _ckpt(fn, *args):
     pf = padding_free()
     return checkpoint.checkpoint(fn, *args, use_reentrant=False,
                                  context_fn=lambda: (contextlib.nullcontext(), no_padding(pf)))
+
+
+def _inert(m) -> bool:
+    """An nn.Dropout that changes nothing now (p = 0 or eval), or Identity."""
+    return isinstance(m, nn.Identity) or (isinstance(m, nn.Dropout) and (m.p == 0.0 or not m.training))
 
 
 class Transformer(nn.Module):
@@ -375,9 +381,19 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return add_norm(self.norm2, src, self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, key_padding_mask=None):
-        src2 = self.self_attn(query=self.with_pos_embed(src, pos), reference_points=reference_points, value=src,
-                              spatial_shapes=spatial_shapes, level_start_index=level_start_index,
-                              key_padding_mask=key_padding_mask)
+        query = self.with_pos_embed(src, pos)
+        sa = self.self_attn
+        if sa.identity_add and sa.batch_first and _inert(self.dropout1):
+            # norm1(src + dropout1(dropout(msda(query)) + query)) with dropout1
+            # inert: the module's dropout and identity add folded into the
+            # add + LayerNorm kernel (gdino_amd.layernorm.add_norm3)
+            out = msda_attend(sa, query, src, reference_points, spatial_shapes, level_start_index,
+                              key_padding_mask, sa.num_heads, sa.num_levels, sa.num_points, sa.im2col_step)
+            y = add_norm3(self.norm1, src, query, out, sa.dropout)
+            src = y if y is not None else add_norm(self.norm1, src, sa.dropout(out) + query)
+            return self.forward_ffn(src)
+        src2 = sa(query=query, reference_points=reference_points, value=src, spatial_shapes=spatial_shapes,
+                  level_start_index=level_start_index, key_padding_mask=key_padding_mask)
         src = add_norm(self.norm1, src, self.dropout1(src2))
         return self.forward_ffn(src)
 
@@ -441,11 +457,21 @@ class DeformableTransformerDecoderLayer(nn.Module):
             tgt2 = self.ca_text(self.with_pos_embed(tgt, tgt_query_pos), text_kv, text_kv,
                                 key_padding_mask=text_attention_mask)[0]
             tgt = add_norm(self.catext_norm, tgt, self.catext_dropout(tgt2))
-        tgt2 = self.cross_attn(query=self.with_pos_embed(tgt, tgt_query_pos).transpose(0, 1),
-                               reference_points=tgt_reference_points.transpose(0, 1).contiguous(),
-                               value=memory.transpose(0, 1), spatial_shapes=memory_spatial_shapes,
-                               level_start_index=memory_level_start_index,
-                               key_padding_mask=memory_key_padding_mask).transpose(0, 1)
+        query = self.with_pos_embed(tgt, tgt_query_pos)
+        ca = self.cross_attn
+        ref_t = tgt_reference_points.transpose(0, 1).contiguous()
+        if ca.identity_add and ca.batch_first and _inert(self.dropout1):
+            # the MSDA module's dropout and identity add folded into norm1
+            # (as in the encoder layer; the output arrives batch-first)
+            out = msda_attend(ca, query.transpose(0, 1), memory.transpose(0, 1), ref_t, memory_spatial_shapes,
+                              memory_level_start_index, memory_key_padding_mask, ca.num_heads, ca.num_levels,
+                              ca.num_points, ca.im2col_step).transpose(0, 1)
+            y = add_norm3(self.norm1, tgt, query, out, ca.dropout)
+            tgt = y if y is not None else add_norm(self.norm1, tgt, ca.dropout(out) + query)
+            return self.forward_ffn(tgt)
+        tgt2 = ca(query=query.transpose(0, 1), reference_points=ref_t, value=memory.transpose(0, 1),
+                  spatial_shapes=memory_spatial_shapes, level_start_index=memory_level_start_index,
+                  key_padding_mask=memory_key_padding_mask).transpose(0, 1)
         tgt = add_norm(self.norm1, tgt, self.dropout1(tgt2))
         return self.forward_ffn(tgt)
 

@@ -842,6 +842,46 @@ def test_emulated_add_layernorm(rows, C, xd, rd):
     assert E.rel_err(db, bd.grad) < 1e-5
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_emulated_add_norm3_matches_the_composition(p):
+    """layernorm.add_norm3 = norm(x + (r + dropout(r2))) (the MSDA identity
+    add and dropout folded into add + LayerNorm) vs the module composition
+    through autograd, fp32 residual / identity, bf16 branch.  p > 0: the mask
+    is regenerated in the backward; the kept set read off the branch
+    gradient (non-zero where kept) drives the composition, and about p of
+    the elements are dropped."""
+    from emu_product import emulated_product
+    from gdino_amd.layernorm import add_norm3
+    g = torch.Generator().manual_seed(5)
+    rows = 300
+    norm = torch.nn.LayerNorm(256)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(256, generator=g))
+        norm.bias.copy_(torch.randn(256, generator=g))
+    drop = torch.nn.Dropout(p)
+    x0 = torch.randn(2, rows // 2, 256, generator=g)
+    r0 = torch.randn(2, rows // 2, 256, generator=g)
+    r20 = torch.randn(2, rows // 2, 256, generator=g).to(torch.bfloat16)
+    dy = torch.randn(2, rows // 2, 256, generator=g)
+    x, r, r2 = (t.clone().requires_grad_(True) for t in (x0, r0, r20))
+    with emulated_product():
+        y = add_norm3(norm, x, r, r2, drop)
+        assert y is not None
+        y.backward(dy)
+    keep = r2.grad != 0 if p > 0 else torch.ones_like(r20, dtype=torch.bool)
+    if p > 0:
+        assert abs(float((~keep).float().mean()) - p) < 0.01
+    xc, rc, r2c = (t.clone().requires_grad_(True) for t in (x0, r0, r20))
+    wc, bc = norm.weight.detach().clone().requires_grad_(True), norm.bias.detach().clone().requires_grad_(True)
+    branch = torch.where(keep, r2c * (1.0 / (1.0 - p)), torch.zeros((), dtype=torch.bfloat16))
+    want = torch.nn.functional.layer_norm(xc + (branch + rc), (256,), wc, bc, norm.eps)
+    want.backward(dy)
+    assert E.rel_err(y.detach(), want.detach()) < 1e-6
+    assert E.rel_err(x.grad, xc.grad) < 1e-5 and E.rel_err(r.grad, rc.grad) < 1e-5
+    assert E.rel_err(r2.grad.float(), r2c.grad.float()) < 1e-2
+    assert E.rel_err(norm.weight.grad, wc.grad) < 1e-5 and E.rel_err(norm.bias.grad, bc.grad) < 1e-5
+
+
 # ------------------------------------------------ box refinement (boxref.hip)
 @pytest.mark.parametrize("dd,transposed_ref,ref_grad", [
     (torch.float32, False, True),
