@@ -444,6 +444,27 @@ gd_status gd_add_layernorm3_backward(const float* x, const float* r, const void*
                                      void* grad_r2_bf16, float* grad_weight, float* grad_bias, void* workspace,
                                      gd_stream_t stream);
 
+/* Pre-norm residual step (Swin blocks, reference swin_transformer.py
+ * :295-296): sum = x + branch * scale, y = LayerNorm(sum) (y_bf16: optional
+ * bf16 twin), x / sum / y fp32 [rows, C], branch fp32 or bf16, scale fp32:
+ * scale[row / tokens_per_sample] when per_sample, else scale[0] (the
+ * drop-path factor).  C in {96, 192, 256, 384, 768}.  Backward sums the two
+ * incoming gradients in the kernel: ds = grad_sum (NULL: 0) + LN'(grad_y);
+ * grad_x = ds, grad_branch = ds * scale (branch dtype, optional), gamma /
+ * beta gradients fp32 (workspace: gd_add_layernorm_workspace_bytes(C)).
+ * Python: gdino_amd.layernorm.add_scaled_norm. */
+gd_status gd_add_scaled_layernorm_forward(const float* x, gd_dtype branch_dtype, const void* branch,
+                                          const float* scale, int64_t tokens_per_sample, int per_sample,
+                                          const float* weight, const float* bias, int64_t rows, int C, float eps,
+                                          float* sum, float* y, void* y_bf16, float* mean, float* rstd,
+                                          gd_stream_t stream);
+gd_status gd_add_scaled_layernorm_backward(const float* grad_sum, const float* grad_y, const float* sum,
+                                           gd_dtype branch_dtype, const float* scale, int64_t tokens_per_sample,
+                                           int per_sample, const float* weight, const float* mean, const float* rstd,
+                                           int64_t rows, int C, float* grad_x, void* grad_branch,
+                                           float* grad_weight, float* grad_bias, void* workspace,
+                                           gd_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Scaled residual ending (fuse_modules.py:285-286, swin_transformer.py:295-296) */
 /* ------------------------------------------------------------------------ */

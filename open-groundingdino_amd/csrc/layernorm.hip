@@ -342,6 +342,143 @@ addln3_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x, con
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pre-norm residual step of the Swin blocks (reference swin_transformer.py
+// :295-296, `x = shortcut + drop_path(attn)` then `norm2(x)`):
+//   s = x + branch * scale,  y = LayerNorm(s)
+// with scale the per-sample drop-path factor (scale[row / n_per]) or one
+// value, both outputs written (s is the residual stream the block adds the
+// MLP to).  Backward takes both incoming gradients and sums them in the
+// kernel: ds = g_s + LN'(g_y); dx = ds, d branch = ds * scale (branch dtype)
+// -- the accumulation add autograd ran between the LayerNorm backward and
+// the residual one, and that residual backward, folded away.
+template <typename TB, int C>
+__global__ void __launch_bounds__(256)
+addsln_fwd_kernel(const float* __restrict__ x, const TB* __restrict__ br, const float* __restrict__ scale,
+                  int64_t n_per, int per_sample, const float* __restrict__ w, const float* __restrict__ b,
+                  int64_t rows, float eps, float* __restrict__ sum_out, float* __restrict__ y,
+                  uint16_t* __restrict__ y16, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int E = (C + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  float wv[E], bv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const bool ok = col_ok<C>(lane, e);
+    wv[e] = ok ? w[lane + 64 * e] : 1.f;
+    bv[e] = ok ? b[lane + 64 * e] : 0.f;
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    const float sc = scale[per_sample ? row / n_per : 0];
+    float s[E];
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      s[e] = col_ok<C>(lane, e) ? x[o] + ldv<TB>(br + o) * sc : 0.f;
+      sum += s[e];
+    }
+    const float mean = wsum(sum) / float(C);
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float d = col_ok<C>(lane, e) ? s[e] - mean : 0.f;
+      sq += d * d;
+    }
+    const float rstd = rsqrtf(wsum(sq) / float(C) + eps);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (!col_ok<C>(lane, e)) continue;
+      const int64_t o = row * C + lane + 64 * e;
+      const float v = (s[e] - mean) * rstd * wv[e] + bv[e];
+      sum_out[o] = s[e];
+      y[o] = v;
+      if (y16) y16[o] = f32_to_bf16(v);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <typename TB, int C>
+__global__ void __launch_bounds__(256)
+addsln_bwd_kernel(const float* __restrict__ g_s, const float* __restrict__ g_y, const float* __restrict__ s_in,
+                  const float* __restrict__ scale, int64_t n_per, int per_sample, const float* __restrict__ w,
+                  const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows,
+                  float* __restrict__ dx, TB* __restrict__ dbr, float* __restrict__ part_w,
+                  float* __restrict__ part_b) {
+  constexpr int E = (C + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  float wv[E], gw[E], gb[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    wv[e] = col_ok<C>(lane, e) ? w[lane + 64 * e] : 1.f;
+    gw[e] = gb[e] = 0.f;
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[E], g[E];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t o = row * C + lane + 64 * e;
+      const bool ok = col_ok<C>(lane, e);
+      xh[e] = ok ? (s_in[o] - mean) * rstd : 0.f;
+      const float d = ok ? g_y[o] : 0.f;
+      gw[e] += d * xh[e];
+      gb[e] += d;
+      g[e] = d * wv[e];
+      sg += g[e];
+      sgx += g[e] * xh[e];
+    }
+    const float mg = wsum(sg) / float(C), mgx = wsum(sgx) / float(C);
+    const float sc = scale[per_sample ? row / n_per : 0];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (!col_ok<C>(lane, e)) continue;
+      const int64_t o = row * C + lane + 64 * e;
+      const float ds = rstd * (g[e] - mg - xh[e] * mgx) + (g_s ? g_s[o] : 0.f);
+      dx[o] = ds;
+      if (dbr) stv<TB>(dbr + o, ds * sc);
+    }
+  }
+  __shared__ float red[2][4][C];
+  const int wv_i = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (!col_ok<C>(lane, e)) continue;
+    red[0][wv_i][lane + 64 * e] = gw[e];
+    red[1][wv_i][lane + 64 * e] = gb[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part_w[int64_t(blockIdx.x) * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    part_b[int64_t(blockIdx.x) * C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+template <typename Fn>
+gd_status dispatch_sln(gd_dtype tb, int C, Fn&& fn) {
+  GD_REQUIRE(tb == GD_F32 || tb == GD_BF16, "add_scaled_layernorm: branch dtype %d (F32, BF16)", int(tb));
+  GD_REQUIRE(C == 96 || C == 192 || C == 256 || C == 384 || C == 768,
+             "add_scaled_layernorm: C=%d not supported (96, 192, 256, 384, 768)", C);
+  auto with_c = [&](auto tag) {
+    switch (C) {
+      case 96: fn(tag, std::integral_constant<int, 96>{}); break;
+      case 192: fn(tag, std::integral_constant<int, 192>{}); break;
+      case 256: fn(tag, std::integral_constant<int, 256>{}); break;
+      case 384: fn(tag, std::integral_constant<int, 384>{}); break;
+      default: fn(tag, std::integral_constant<int, 768>{}); break;
+    }
+  };
+  if (tb == GD_BF16) with_c(uint16_t{});
+  else with_c(float{});
+  return GD_OK;
+}
+
 Drop3 make_drop3(float p, uint32_t seed, const uint32_t* seed_dev) {
   Drop3 d;
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -512,5 +649,60 @@ extern "C" gd_status gd_add_layernorm3_backward(const float* x, const float* r, 
   hipLaunchKernelGGL(addln_reduce_kernel, dim3(unsigned((C + 15) / 16)), dim3(1024), 0, s, part_w, part_b, kLnBlocks,
                      C, grad_weight, grad_bias);
   GD_LAUNCH_CHECK("add_layernorm3_reduce");
+  return GD_OK;
+}
+
+extern "C" gd_status gd_add_scaled_layernorm_forward(const float* x, gd_dtype branch_dtype, const void* branch,
+                                                    const float* scale, int64_t tokens_per_sample, int per_sample,
+                                                    const float* weight, const float* bias, int64_t rows, int C,
+                                                    float eps, float* sum, float* y, void* y_bf16, float* mean,
+                                                    float* rstd, gd_stream_t stream) {
+  GD_REQUIRE(rows >= 0 && (!per_sample || tokens_per_sample > 0), "add_scaled_layernorm: rows=%lld n=%lld",
+             (long long)rows, (long long)tokens_per_sample);
+  if (rows == 0) return GD_OK;
+  GD_REQUIRE(x && branch && scale && weight && bias && sum && y && mean && rstd,
+             "add_scaled_layernorm_forward: null pointer");
+  const int64_t blocks64 = (rows + 3) / 4;
+  const unsigned blocks = unsigned(blocks64 < 8192 ? blocks64 : 8192);
+  hipStream_t s = as_hip(stream);
+  gd_status st = dispatch_sln(branch_dtype, C, [&](auto tb, auto c) {
+    using TB = decltype(tb);
+    hipLaunchKernelGGL((addsln_fwd_kernel<TB, decltype(c)::value>), dim3(blocks), dim3(256), 0, s, x,
+                       (const TB*)branch, scale, tokens_per_sample, per_sample, weight, bias, rows, eps, sum, y,
+                       (uint16_t*)y_bf16, mean, rstd);
+  });
+  if (st != GD_OK) return st;
+  GD_LAUNCH_CHECK("add_scaled_layernorm_fwd");
+  return GD_OK;
+}
+
+extern "C" gd_status gd_add_scaled_layernorm_backward(const float* grad_sum, const float* grad_y, const float* sum,
+                                                     gd_dtype branch_dtype, const float* scale,
+                                                     int64_t tokens_per_sample, int per_sample, const float* weight,
+                                                     const float* mean, const float* rstd, int64_t rows, int C,
+                                                     float* grad_x, void* grad_branch, float* grad_weight,
+                                                     float* grad_bias, void* workspace, gd_stream_t stream) {
+  GD_REQUIRE(rows >= 0, "add_scaled_layernorm: rows < 0");
+  GD_REQUIRE(grad_weight && grad_bias && workspace, "add_scaled_layernorm_backward: grad_weight / grad_bias");
+  hipStream_t s = as_hip(stream);
+  if (rows == 0) {
+    GD_HIP_CHECK(fill_u32_async(grad_weight, 0u, sizeof(float) * C, s));
+    GD_HIP_CHECK(fill_u32_async(grad_bias, 0u, sizeof(float) * C, s));
+    return GD_OK;
+  }
+  GD_REQUIRE(grad_y && sum && scale && weight && mean && rstd && grad_x, "add_scaled_layernorm_backward: null pointer");
+  float* part_w = static_cast<float*>(workspace);
+  float* part_b = part_w + int64_t(kLnBlocks) * C;
+  gd_status st = dispatch_sln(branch_dtype, C, [&](auto tb, auto c) {
+    using TB = decltype(tb);
+    hipLaunchKernelGGL((addsln_bwd_kernel<TB, decltype(c)::value>), dim3(kLnBlocks), dim3(256), 0, s, grad_sum,
+                       grad_y, sum, scale, tokens_per_sample, per_sample, weight, mean, rstd, rows, grad_x,
+                       (TB*)grad_branch, part_w, part_b);
+  });
+  if (st != GD_OK) return st;
+  GD_LAUNCH_CHECK("add_scaled_layernorm_bwd");
+  hipLaunchKernelGGL(addln_reduce_kernel, dim3(unsigned((C + 15) / 16)), dim3(1024), 0, s, part_w, part_b, kLnBlocks,
+                     C, grad_weight, grad_bias);
+  GD_LAUNCH_CHECK("add_scaled_layernorm_reduce");
   return GD_OK;
 }

@@ -165,6 +165,84 @@ def add_norm3(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, r2: torch.Te
                                        norm.eps, p, seed, bool(bf16_twin))
 
 
+_lib.register("gd_add_scaled_layernorm_forward", [_p, _i, _p, _p, _i64, _i, _p, _p, _i64, _i, _f, _p, _p, _p, _p,
+                                                   _p, _p])
+_lib.register("gd_add_scaled_layernorm_backward", [_p, _p, _p, _i, _p, _i64, _i, _p, _p, _p, _i64, _i, _p, _p, _p,
+                                                    _p, _p, _p])
+SLN_WIDTHS = (96, 192, 256, 384, 768)
+
+
+class AddScaledNormFunction(torch.autograd.Function):
+    """(sum, y) = (x + branch * scale, LayerNorm(x + branch * scale)) with a
+    per-sample (or single) fp32 scale that carries no gradient
+    (csrc/layernorm.hip addsln_*).  The backward receives both gradients and
+    sums them inside the kernel."""
+
+    @staticmethod
+    def forward(ctx, x, branch, scale, per_sample, weight, bias, eps, twin=True):
+        c = x.shape[-1]
+        rows = x.numel() // c
+        n_per = rows // x.shape[0] if per_sample else 1
+        s = torch.empty_like(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        y16 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if _bf16_twin_wanted(x, twin) else None
+        _lib.call("gd_add_scaled_layernorm_forward", x.data_ptr(), _lib.dtype_code(branch), branch.data_ptr(),
+                  scale.data_ptr(), n_per, int(per_sample), weight.data_ptr(), bias.data_ptr(), rows, c, float(eps),
+                  s.data_ptr(), y.data_ptr(), _lib.ptr(y16), mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(x),
+                  nbytes=rows * (c * (4 + branch.element_size() + 4 + 4 + (0 if y16 is None else 2)) + 8))
+        if y16 is not None:
+            y._gd_bf16 = (y16, y._version)
+        ctx.save_for_backward(s, scale, weight, mean, rstd)
+        ctx.meta = (per_sample, n_per, branch.dtype)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, g_s, g_y):
+        s, scale, weight, mean, rstd = ctx.saved_tensors
+        per_sample, n_per, bdt = ctx.meta
+        c = s.shape[-1]
+        rows = s.numel() // c
+        g_y = torch.zeros_like(s) if g_y is None else g_y.float().contiguous()
+        g_s = None if g_s is None else g_s.float().contiguous()
+        dx = torch.empty_like(s)
+        db_ = torch.empty(s.shape, dtype=bdt, device=s.device) if ctx.needs_input_grad[1] else None
+        dw = torch.empty(c, dtype=torch.float32, device=s.device)
+        dbias = torch.empty(c, dtype=torch.float32, device=s.device)
+        ws = _workspace(c, s.device)
+        _lib.call("gd_add_scaled_layernorm_backward", _lib.ptr(g_s), g_y.data_ptr(), s.data_ptr(),
+                  _lib._DTYPE_CODE[bdt], scale.data_ptr(), n_per, int(per_sample),
+                  weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, c, dx.data_ptr(), _lib.ptr(db_),
+                  dw.data_ptr(), dbias.data_ptr(), ws.data_ptr(), _lib.stream_of(s),
+                  nbytes=rows * (c * (4 * 4 + (2 if db_ is not None else 0)) + 8))
+        return (dx if ctx.needs_input_grad[0] else None, db_, None, None,
+                dw if ctx.needs_input_grad[4] else None, dbias if ctx.needs_input_grad[5] else None, None, None)
+
+
+def add_scaled_norm(norm: nn.LayerNorm, x: torch.Tensor, branch: torch.Tensor, drop_prob: float = 0.0,
+                    training: bool = False, bf16_twin: bool = True):
+    """(x + drop_path(branch), norm(x + drop_path(branch))) as one kernel
+    each way (the Swin blocks' attention residual and norm2, reference
+    swin_transformer.py:295-296), the per-sample drop-path mask drawn as
+    misc.add_drop_path draws it.  None when not applicable (the caller runs
+    add_drop_path + layer_norm)."""
+    c = x.shape[-1]
+    if not (supported(norm, x, None) and c in SLN_WIDTHS and x.dtype == torch.float32 and x.shape == branch.shape
+            and branch.dtype in (torch.float32, torch.bfloat16) and x.dim() == 3):
+        return None
+    from .misc import device_const
+    if drop_prob > 0.0 and training:
+        keep = 1.0 - drop_prob
+        mask = torch.empty((branch.shape[0], 1, 1), dtype=branch.dtype, device=branch.device).bernoulli_(keep)
+        scale, per_sample = mask.div_(keep).float().reshape(-1), True
+    else:
+        scale = device_const(("unit_scale",), lambda: torch.ones(1, dtype=torch.float32), x.device)
+        per_sample = False
+    return AddScaledNormFunction.apply(x.contiguous(), branch.contiguous(), scale, per_sample, norm.weight,
+                                       norm.bias, norm.eps, bool(bf16_twin))
+
+
 def layer_norm(norm: nn.LayerNorm, x: torch.Tensor, bf16_twin: bool = True) -> torch.Tensor:
     """norm(x) with no residual (Swin's pre-norms and patch-merging norm,
     swin_transformer.py:245, 296, 357): the same kernels with a NULL residual,

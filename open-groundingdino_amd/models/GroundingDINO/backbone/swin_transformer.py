@@ -23,7 +23,7 @@ import torch.utils.checkpoint as checkpoint
 
 from gdino_amd.conv import GemmConv2d
 from gdino_amd import castcache, kernels
-from gdino_amd.layernorm import layer_norm
+from gdino_amd.layernorm import add_scaled_norm, layer_norm
 from gdino_amd.misc import DropPath, NestedTensor, add_drop_path, to_2tuple, trunc_normal_
 
 
@@ -128,13 +128,16 @@ class SwinTransformerBlock(nn.Module):
         self.mlp = Mlp(dim, int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
         self.H = self.W = None
 
-    def forward(self, x, mask_matrix):
+    def forward(self, x, mask_matrix, normed=None, next_norm=None):
+        """normed: norm1(x) when the previous block computed it (its fused MLP
+        residual + this block's norm1); next_norm: the following block's
+        norm1, to return (x_out, next_norm(x_out)) from one fused kernel."""
         b, length, c = x.shape
         h, w = self.H, self.W
         assert length == h * w, "input feature has wrong size"
         ws, sh = self.window_size, self.shift_size
         shortcut = x
-        x = layer_norm(self.norm1, x)
+        x = layer_norm(self.norm1, x) if normed is None else normed
         attn = self.attn
         if attn.attn_drop.p > 0.0 and self.training:
             x = self._windowed_attention(x, mask_matrix)
@@ -147,10 +150,23 @@ class SwinTransformerBlock(nn.Module):
                                                attn.relative_position_index.view(-1), mask_matrix, (h, w), ws, sh,
                                                attn.scale)
             x = attn.proj_drop(attn.proj(x))
-        # x + drop_path(branch) as one kernel each (misc.add_drop_path)
+        # x + drop_path(branch) as one kernel each (misc.add_drop_path); the
+        # attention residual and norm2 as one kernel each way, whose backward
+        # also sums the two gradients of x (layernorm.add_scaled_norm)
         dp = self.drop_path.drop_prob if isinstance(self.drop_path, DropPath) else 0.0
+        fused = add_scaled_norm(self.norm2, shortcut, x, dp, self.training)
+        if fused is not None:
+            x, y = fused
+            if next_norm is not None:
+                # the MLP residual and the next block's norm1 likewise
+                nxt = add_scaled_norm(next_norm, x, self.mlp(y), dp, self.training)
+                if nxt is not None:
+                    return nxt
+                return add_drop_path(x, self.mlp(y), dp, self.training), None
+            return add_drop_path(x, self.mlp(y), dp, self.training)
         x = add_drop_path(shortcut, x, dp, self.training)
-        return add_drop_path(x, self.mlp(layer_norm(self.norm2, x)), dp, self.training)
+        out = add_drop_path(x, self.mlp(layer_norm(self.norm2, x)), dp, self.training)
+        return (out, None) if next_norm is not None else out
 
     def _windowed_attention(self, x, mask_matrix):
         """reference :250-290 step by step (the path with attention dropout)"""
@@ -246,12 +262,17 @@ class BasicLayer(nn.Module):
         ws = self.window_size
         hp, wp = -(-h // ws) * ws, -(-w // ws) * ws
         mask = shifted_window_mask(hp, wp, ws, self.shift_size, x.device)
-        for blk in self.blocks:
+        normed = None
+        for i, blk in enumerate(self.blocks):
             blk.H, blk.W = h, w
+            # block i's MLP residual also normalises for block i + 1 (one
+            # fused kernel each way, layernorm.add_scaled_norm)
+            nxt = self.blocks[i + 1].norm1 if i + 1 < len(self.blocks) else None
             if self.use_checkpoint and torch.is_grad_enabled():
-                x = checkpoint.checkpoint(blk, x, mask, use_reentrant=False)
+                out = checkpoint.checkpoint(blk, x, mask, normed, nxt, use_reentrant=False)
             else:
-                x = blk(x, mask)
+                out = blk(x, mask, normed, nxt)
+            x, normed = out if nxt is not None else (out, None)
         if self.downsample is not None:
             return x, h, w, self.downsample(x, h, w), (h + 1) // 2, (w + 1) // 2
         return x, h, w, x, h, w

@@ -174,7 +174,10 @@ class Transformer(nn.Module):
             # top-k indices are used (gdino_amd/contrastive.py)
             topk_logits = kernels.contrastive_rowmax(output_memory, text_dict["encoded_text"],
                                                      text_dict["text_token_mask"])
-            enc_coord = self.enc_out_bbox_embed(output_memory) + output_proposals
+            # (the bf16 head output widened first: a mixed bf16 + fp32 add of
+            # this [B, S, 4] shape took 90 us in PyTorch's templated kernel)
+            delta = self.enc_out_bbox_embed(output_memory)
+            enc_coord = delta.to(torch.promote_types(delta.dtype, output_proposals.dtype)) + output_proposals
             topk_proposals = topk_indices(topk_logits, self.num_queries)  # [bs, nq]
             idx4 = topk_proposals.unsqueeze(-1).expand(-1, -1, 4)
             refpoint_embed_undetach = torch.gather(enc_coord, 1, idx4)
@@ -297,6 +300,42 @@ class TransformerEncoder(nn.Module):
         return output, memory_text
 
 
+# GDINO_DEFER_BOX_REFINE=0: the per-layer anchor update with autograd (A/B)
+DEFER_BOX_REFINE = os.environ.get("GDINO_DEFER_BOX_REFINE", "1") != "0"
+
+
+class _BatchedBoxRefine(torch.autograd.Function):
+    """The decoder's refined anchors new_ref[l] = box_refine(bbox_embed(
+    out[l]), ref[l]) of every layer (reference transformer.py
+    :728-731) as ONE autograd node: the forward returns the values the layer
+    loop computed without autograd (the same kernels, so the anchors each
+    layer sampled with are exactly these), the backward recomputes the shared
+    bbox_embed MLP once over all layers' queries [L, nq, bs, C] under the
+    forward's autocast state and differentiates it -- one set of GEMMs and
+    one gradient per parameter instead of L of each (plus L - 1
+    accumulations of the shared weights' gradients)."""
+
+    @staticmethod
+    def forward(ctx, values, outs, refs, mlp, *params):
+        dev = outs.device.type
+        ctx.mlp = mlp
+        ctx.amp = (torch.is_autocast_enabled(dev), torch.get_autocast_dtype(dev)) if dev in ("cuda", "cpu") else None
+        ctx.save_for_backward(outs, refs)
+        return values.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        outs, refs = ctx.saved_tensors
+        dev = outs.device.type
+        params = [q for q in ctx.mlp.parameters() if q.requires_grad]
+        amp = ctx.amp if ctx.amp is not None else (False, None)
+        with torch.enable_grad(), torch.autocast(device_type=dev, enabled=amp[0], dtype=amp[1]):
+            x = outs.detach().requires_grad_(True)
+            y = box_refine(ctx.mlp(x), refs)
+        grads = torch.autograd.grad(y, [x] + params, g, allow_unused=True)
+        return (None, grads[0], None, None, *grads[1:])
+
+
 class TransformerDecoder(nn.Module):
     def __init__(self, decoder_layer, num_layers, norm=None, return_intermediate=False, d_model=256,
                  query_dim=4, num_feature_levels=1):
@@ -328,6 +367,11 @@ class TransformerDecoder(nn.Module):
         reference_points = refpoints_unsigmoid.sigmoid()
         ref_points = [reference_points]
         vr = torch.cat([valid_ratios, valid_ratios], -1) if reference_points.shape[-1] == 4 else valid_ratios
+        # one shared bbox_embed (dec_pred_bbox_embed_share, the cfg default)
+        # and autograd on: the per-layer anchor updates' backward runs batched
+        deferred = ([] if (DEFER_BOX_REFINE and self.bbox_embed is not None and torch.is_grad_enabled()
+                           and all(m is self.bbox_embed[0] for m in self.bbox_embed)
+                           and not refpoints_unsigmoid.requires_grad) else None)
         for layer_id, layer in enumerate(self.layers):
             # ref_input [nq, bs, nlevel, 4], query_sine_embed [nq, bs, 512]
             ref_input, query_sine_embed = query_anchors(reference_points, vr)
@@ -350,10 +394,29 @@ class TransformerDecoder(nn.Module):
                 print(f"output layer_id {layer_id} is nan: num_nan {int(output.isnan().sum())}, "
                       f"num_inf {int(output.isinf().sum())}")
             if self.bbox_embed is not None:
-                new_ref = box_refine(self.bbox_embed[layer_id](output), reference_points)  # transformer.py:728-731
-                reference_points = new_ref.detach()
+                if deferred is not None:
+                    # the anchor update without autograd; its gradient path
+                    # is rebuilt for all layers at once below
+                    with torch.no_grad():
+                        new_ref = box_refine(self.bbox_embed[layer_id](output), reference_points)
+                    deferred.append((output, reference_points, new_ref))
+                else:
+                    new_ref = box_refine(self.bbox_embed[layer_id](output), reference_points)  # transformer.py:728-731
                 ref_points.append(new_ref)
+                reference_points = new_ref.detach()
             intermediate.append(self.norm(output))
+        if deferred:
+            # every layer's refined anchors through ONE batched bbox_embed on
+            # the gradient path (_BatchedBoxRefine); the last layer's too (the
+            # model's box heads read reference[:-1], other callers of the
+            # module may use all of them)
+            n = len(deferred)
+            outs = torch.stack([d[0] for d in deferred])
+            refs = torch.stack([d[1] for d in deferred])
+            vals = torch.stack([d[2] for d in deferred])
+            mlp = self.bbox_embed[0]
+            params = [q for q in mlp.parameters() if q.requires_grad]
+            ref_points[1:1 + n] = list(_BatchedBoxRefine.apply(vals, outs, refs, mlp, *params).unbind(0))
         return [[x.transpose(0, 1) for x in intermediate], [r.transpose(0, 1) for r in ref_points]]
 
 

@@ -882,6 +882,44 @@ def test_emulated_add_norm3_matches_the_composition(p):
     assert E.rel_err(norm.weight.grad, wc.grad) < 1e-5 and E.rel_err(norm.bias.grad, bc.grad) < 1e-5
 
 
+@pytest.mark.parametrize("C,bd,dp", [(96, torch.bfloat16, 0.0), (192, torch.float32, 0.2), (384, torch.bfloat16, 0.3),
+                                      (768, torch.bfloat16, 0.0)])
+def test_emulated_add_scaled_norm_matches_the_composition(C, bd, dp):
+    """layernorm.add_scaled_norm = (x + drop_path(branch), norm(...)) vs
+    add_drop_path + layer_norm through autograd, the same seeded drop-path
+    draw, both outputs consumed (the backward sums their gradients in the
+    kernel)."""
+    from emu_product import emulated_product
+    from gdino_amd.layernorm import add_scaled_norm
+    from gdino_amd.misc import add_drop_path
+    g = torch.Generator().manual_seed(C)
+    norm = torch.nn.LayerNorm(C)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(C, generator=g))
+        norm.bias.copy_(torch.randn(C, generator=g))
+    x0 = torch.randn(3, 50, C, generator=g)
+    b0 = torch.randn(3, 50, C, generator=g).to(bd)
+    gs, gy = torch.randn(3, 50, C, generator=g), torch.randn(3, 50, C, generator=g)
+    out = {}
+    for fused in (True, False):
+        x, b = x0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        norm.zero_grad()
+        torch.manual_seed(11)
+        with emulated_product():
+            if fused:
+                r = add_scaled_norm(norm, x, b, dp, True)
+                assert r is not None
+                s, y = r
+            else:
+                s = add_drop_path(x, b, dp, True)
+                y = torch.nn.functional.layer_norm(s, (C,), norm.weight, norm.bias, norm.eps)
+            ((s * gs).sum() + (y * gy).sum()).backward()
+        out[fused] = (s.detach(), y.detach(), x.grad, b.grad, norm.weight.grad.clone(), norm.bias.grad.clone())
+    for a, w in zip(out[True], out[False]):
+        assert a.dtype == w.dtype
+        assert E.rel_err(a.float(), w.float()) < (1e-2 if a.dtype == torch.bfloat16 else 2e-5)
+
+
 # ------------------------------------------------ box refinement (boxref.hip)
 @pytest.mark.parametrize("dd,transposed_ref,ref_grad", [
     (torch.float32, False, True),
