@@ -576,6 +576,15 @@ const char* gd_runtime_info(void);
  * buffer instead of faulting); this call is how the host learns of it.
  * Not for use inside a graph capture (it synchronises). */
 gd_status gd_device_status(gd_stream_t stream);
+/* Token-linear forward GEMM (csrc/tlin.hip): y[M, N] = x[M, K] . W[N, K]^T
+ * (+ bias[N]) (ReLU when relu != 0), bf16 x / W / bias / y, fp32
+ * accumulation; x rows ldx apart, y rows ldy apart (elements, multiples of
+ * 8, 16-B aligned), W contiguous.  K, N multiples of 8.  The forward of the
+ * token-heavy Linear layers (reference F.linear under bf16 autocast:
+ * transformer.py:784-808, fuse_modules.py:43-64, swin_transformer.py:30-46).
+ * Python: gdino_amd.wgrad.TokenLinear. */
+gd_status gd_token_linear_forward(const void* x, int64_t ldx, const void* weight, const void* bias, int M, int K,
+                                  int N, int relu, void* y, int64_t ldy, gd_stream_t stream);
 /* ABI version: bumped when a signature changes. */
 int gd_abi_version(void);
 

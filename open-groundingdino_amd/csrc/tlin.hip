@@ -1,0 +1,197 @@
+// Token-linear forward GEMM for gfx950:  y[M, N] = x[M, K] . W[N, K]^T (+ b)
+// (+ ReLU), bf16 operands, fp32 accumulation, bf16 output -- the forward of
+// the encoder / fusion / Swin Linear layers (TokenLinear, gdino_amd/wgrad.py)
+// over M = tens of thousands of tokens with K, N = 96..2048.
+//
+// Why a kernel of our own: on these tall-skinny shapes the library GEMM
+// runs at 1.5-3.2 TB/s, 2.5-5x its HBM floor (tools/probes/gemm_shapes.py,
+// profiles/r05m_gemm_shapes.jsonl: [44 446 x 256] x [256 x 384] 24 us for
+// 7 us of bytes, Swin-T stage 0's K = 96 at 5.4x).  With K <= 2048 the whole
+// reduction of a 128 x 128 output tile is a short loop, so the tile is
+// memory-fed: W (<= 8 MB) stays in L2, x is streamed once per N tile.
+//
+// Tile 128 (tokens) x 128 (outputs), 256 threads = 4 waves of 64 x 64, each
+// 4 x 4 v_mfma_f32_16x16x32_bf16 blocks.  K in chunks of 64: a chunk of x
+// and of W is loaded with 16-B vector loads (8 lanes per 128-B row: whole
+// cache lines) into registers, stored to an LDS stage (row pitch 72
+// elements: 16 consecutive rows' 16-B fragment reads hit 64 distinct banks),
+// and the next chunk's loads are in flight while this one is multiplied
+// (two stages).  Fragments are natural-order rows (mfma_frag.inc: lane
+// (c, g) holds k = 8g..8g+7 of row c), no transposes: both operands are
+// K-contiguous.  Epilogue: + bias, ReLU, bf16, staged through LDS so that
+// each output row leaves as 16-B stores.  Rows >= M, outputs >= N and
+// k >= K are zero-filled on load and masked on store (M, N, K multiples of
+// nothing but 8 -- N and K for the 16-B vectors).
+//
+// Grid: one workgroup per tile, tiles ordered (m, n) with n fastest and
+// remapped so that each XCD runs a contiguous range (the N tiles of an M
+// block share the XCD's L2 copy of its x rows).
+#include "gd_common.h"
+
+namespace gd {
+namespace {
+#include "mfma_frag.inc"
+
+constexpr int kTlM = 128, kTlN = 128, kTlK = 64;
+constexpr int kTlPitch = kTlK + 8;                  // LDS row pitch (elements)
+constexpr int kTlStage = (kTlM + kTlN) * kTlPitch;  // one stage: x rows, then W rows
+constexpr int kTlOutPitch = kTlN + 8;               // epilogue staging pitch (bf16 elements)
+static_assert(kTlM * kTlOutPitch <= 2 * kTlStage, "epilogue staging fits the stages");
+
+__device__ __forceinline__ int tl_xcd_logical(int h, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = h % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + h / 8;
+}
+
+template <bool RELU, bool BIAS>
+__global__ void __launch_bounds__(256)
+tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ w,
+                const uint16_t* __restrict__ bias, int M, int K, int N, uint16_t* __restrict__ y, int64_t ldy,
+                int tiles_n) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kTlStage];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int L = tl_xcd_logical(int(blockIdx.x), int(gridDim.x));
+  const int m0 = (L / tiles_n) * kTlM, n0 = (L % tiles_n) * kTlN;
+
+  // loader: vector v = tid + 256 h (h < 4) of a [128 rows][8 x 16 B] chunk;
+  // two chunks in registers (P = 0 / 1): chunk kc + 2 is loading while
+  // chunk kc + 1 waits in registers and chunk kc is multiplied
+  const int lpart = tid & 7, lrow = tid >> 3;  // rows lrow + 32 h
+  uint4 rx[2][4], rw[2][4];
+  auto load = [&](int p, int k0) {
+    const int k = k0 + 8 * lpart;
+    const bool kok = k < K;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int r = lrow + 32 * h;
+      const int mr = m0 + r, nr = n0 + r;
+      rx[p][h] = (kok && mr < M) ? *reinterpret_cast<const uint4*>(x + int64_t(mr) * ldx + k)
+                                 : make_uint4(0, 0, 0, 0);
+      rw[p][h] = (kok && nr < N) ? *reinterpret_cast<const uint4*>(w + int64_t(nr) * K + k)
+                                 : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto stash = [&](int p, int buf) {
+    uint16_t* xs = lds + buf * kTlStage;
+    uint16_t* ws = xs + kTlM * kTlPitch;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int r = lrow + 32 * h;
+      *reinterpret_cast<uint4*>(xs + r * kTlPitch + 8 * lpart) = rx[p][h];
+      *reinterpret_cast<uint4*>(ws + r * kTlPitch + 8 * lpart) = rw[p][h];
+    }
+  };
+
+  gd_f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
+
+  const int nchunks = (K + kTlK - 1) / kTlK;
+  load(0, 0);
+  if (nchunks > 1) load(1, kTlK);
+  for (int kc = 0, buf = 0; kc < nchunks; ++kc, buf ^= 1) {
+    // (register sets alternate with kc; the compiler keeps the unrolled
+    // pair's indices static)
+    if (kc & 1) {
+      stash(1, buf);
+      if (kc + 2 < nchunks) load(1, (kc + 2) * kTlK);
+    } else {
+      stash(0, buf);
+      if (kc + 2 < nchunks) load(0, (kc + 2) * kTlK);
+    }
+    __syncthreads();
+    const uint16_t* xs = lds + buf * kTlStage;
+    const uint16_t* ws = xs + kTlM * kTlPitch;
+#pragma unroll
+    for (int s = 0; s < kTlK / 32; ++s) {
+      WFrag<uint16_t> af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i].v = *reinterpret_cast<const gd_bf16x8*>(xs + (64 * wm + 16 * i + c) * kTlPitch + 32 * s + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[j].v = *reinterpret_cast<const gd_bf16x8*>(ws + (64 * wn + 16 * j + c) * kTlPitch + 32 * s + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = wmma(af[i], bf[j], acc[i][j]);
+    }
+  }
+
+  // epilogue: acc[i][j][r] = y[m0 + 64 wm + 16 i + 4 g + r][n0 + 64 wn + 16 j + c]
+  __syncthreads();  // every wave's last fragment reads are done
+  uint16_t* ot = lds;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = 64 * wn + 16 * j + c;
+    float bv = 0.f;
+    if (BIAS && n0 + col < N) bv = bf16_to_f32(bias[n0 + col]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] + bv;
+        if (RELU) v = v > 0.f ? v : 0.f;
+        ot[(64 * wm + 16 * i + 4 * g + r) * kTlOutPitch + col] = f32_to_bf16(v);
+      }
+  }
+  __syncthreads();
+  // 128 rows x 16 vectors of 8 outputs; 16 lanes per row
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    const int v = tid + 256 * h;
+    const int row = v >> 4, part = v & 15;
+    const int mr = m0 + row, col = n0 + 8 * part;
+    if (mr < M && col < N)
+      *reinterpret_cast<uint4*>(y + int64_t(mr) * ldy + col) =
+          *reinterpret_cast<const uint4*>(ot + row * kTlOutPitch + 8 * part);
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+}  // namespace gd
+
+using namespace gd;
+
+extern "C" gd_status gd_token_linear_forward(const void* x, int64_t ldx, const void* weight, const void* bias,
+                                            int M, int K, int N, int relu, void* y, int64_t ldy,
+                                            gd_stream_t stream) {
+  GD_REQUIRE(M >= 0 && K > 0 && N > 0 && K % 8 == 0 && N % 8 == 0,
+             "token_linear: M=%d K=%d N=%d (K, N multiples of 8)", M, K, N);
+  if (M == 0) return GD_OK;
+  GD_REQUIRE(x && weight && y, "token_linear: null pointer");
+  GD_REQUIRE(aligned16(x) && aligned16(weight) && aligned16(y) && ldx % 8 == 0 && ldy % 8 == 0 && ldx >= K &&
+                 ldy >= N,
+             "token_linear: 16-byte aligned rows required (ldx=%lld ldy=%lld)", (long long)ldx, (long long)ldy);
+  const int tiles_m = (M + kTlM - 1) / kTlM, tiles_n = (N + kTlN - 1) / kTlN;
+  GD_REQUIRE(int64_t(tiles_m) * tiles_n < (int64_t(1) << 31), "token_linear: grid too large");
+  const dim3 grid(unsigned(tiles_m * tiles_n));
+  hipStream_t s = as_hip(stream);
+  const uint16_t* xp = static_cast<const uint16_t*>(x);
+  const uint16_t* wp = static_cast<const uint16_t*>(weight);
+  const uint16_t* bp = static_cast<const uint16_t*>(bias);
+  uint16_t* yp = static_cast<uint16_t*>(y);
+  if (relu) {
+    if (bias)
+      hipLaunchKernelGGL((tlin_fwd_kernel<true, true>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
+                         tiles_n);
+    else
+      hipLaunchKernelGGL((tlin_fwd_kernel<true, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
+                         tiles_n);
+  } else {
+    if (bias)
+      hipLaunchKernelGGL((tlin_fwd_kernel<false, true>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
+                         tiles_n);
+    else
+      hipLaunchKernelGGL((tlin_fwd_kernel<false, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
+                         tiles_n);
+  }
+  GD_LAUNCH_CHECK("token_linear_forward");
+  return GD_OK;
+}

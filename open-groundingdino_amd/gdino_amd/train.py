@@ -453,13 +453,22 @@ def build_training(args, device):
     return model, criterion, post, optimizer
 
 
-def small_train_step(device, height=256, width=320, seed=0) -> float:
-    """smoke(): one tiny train step of the full Swin-T + BERT-base model."""
+def small_train_step(device, height=256, width=320, seed=0, stochastic=True) -> float:
+    """smoke(): one tiny train step of the full Swin-T + BERT-base model.
+    stochastic=False zeroes every dropout / drop-path rate, so the loss
+    depends on the weights, the batch and the kernels' rounding only, not on
+    the order the step draws random numbers in (smoke pins it)."""
     from .config import make_args
     torch.manual_seed(seed)
     args = make_args(device=str(device))
     model, criterion, _, opt = build_training(args, device)
     model.train()
+    if not stochastic:
+        for m in model.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+            if hasattr(m, "drop_prob"):
+                m.drop_prob = 0.0
     samples, targets, captions, cats = synthetic_batch(1, height, width, n_boxes=3, n_tokens=24, seed=seed,
                                                        device=device)
     loss = train_step(model, criterion, opt, samples, targets, captions, cats)

@@ -45,6 +45,45 @@ ENABLED = True
 # bf16 -> fp32 cast kernel for each (GDINO_FP32_WGRAD=0: autocast's path)
 FP32_OUT_GEMM = os.environ.get("GDINO_FP32_WGRAD", "1") != "0"
 
+# the forward GEMM of TokenLinear on csrc/tlin.hip (GD_TLIN=0: the library
+# GEMM, A/B); from this many tokens on (below, the library's small-M tiles win)
+_lib.register("gd_token_linear_forward", [_p, _i64, _p, _p, _i, _i, _i, _i, _p, _i64, _p])
+TLIN = os.environ.get("GD_TLIN", "1") != "0"
+TLIN_MIN_TOKENS = 2048
+
+
+def tlin_wins(k: int, n: int) -> bool:
+    """The shapes where the kernel beats the library GEMM
+    (profiles/r05m_gemm_shapes.jsonl): a narrow reduction or output (Swin-T
+    stage 0's K = 96 / N = 96: 40 vs 69 us, 33 vs 55 us); at K, N >= 256 the
+    library's tiles are faster (18 vs 14 us at 256 -> 256)."""
+    return min(k, n) <= TLIN_MAX_NARROW
+
+
+TLIN_MAX_NARROW = 128
+
+
+def tlin_ok(x2: torch.Tensor, wc: torch.Tensor, bc) -> bool:
+    """x2 [M, K] bf16 rows (unit column stride, 16-B aligned), wc [N, K] bf16
+    contiguous, bc None or bf16 [N]; K, N multiples of 8; a winning shape."""
+    m, k = x2.shape
+    n = wc.shape[0]
+    return (TLIN and _lib.enabled("tlin") and _lib.on_device(x2) and m >= TLIN_MIN_TOKENS and tlin_wins(k, n)
+            and x2.dtype == wc.dtype == torch.bfloat16 and (bc is None or (bc.dtype == torch.bfloat16
+                                                                           and bc.is_contiguous()))
+            and wc.is_contiguous() and k % 8 == 0 and n % 8 == 0 and x2.stride(1) == 1 and x2.stride(0) % 8 == 0
+            and x2.data_ptr() % 16 == 0 and wc.data_ptr() % 16 == 0)
+
+
+def tlin_forward(x2: torch.Tensor, wc: torch.Tensor, bc=None, relu: bool = False) -> torch.Tensor:
+    """y [M, N] bf16 = x2 . wc^T (+ bc) (ReLU) on the token-linear kernel."""
+    m, k = x2.shape
+    n = wc.shape[0]
+    y = torch.empty(m, n, dtype=torch.bfloat16, device=x2.device)
+    _lib.call("gd_token_linear_forward", x2.data_ptr(), x2.stride(0), wc.data_ptr(), _lib.ptr(bc), m, k, n,
+              int(relu), y.data_ptr(), y.stride(0), _lib.stream_of(x2), flops=2.0 * m * k * n)
+    return y
+
 
 def eligible(x: torch.Tensor, out_features: int, dtype=None) -> bool:
     """Route a Linear's weight gradient to the split-K kernel: GPU, T >= MIN_TOKENS
@@ -176,7 +215,11 @@ class TokenLinear(torch.autograd.Function):
             # no separate activation pass over the [tokens, d_ffn] output;
             # relu commutes with the bf16 rounding, so the result equals the
             # unfused F.relu(F.linear(...))
-            y = torch._addmm_activation(bc, xc.reshape(-1, xc.shape[-1]), wc.t(), use_gelu=False)
+            x2 = xc.reshape(-1, xc.shape[-1])
+            if tlin_ok(x2, wc, bc):
+                y = tlin_forward(x2, wc, bc, relu=True)
+            else:
+                y = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
             y = y.view(*xc.shape[:-1], wc.shape[0])
             ctx.save_for_backward(xc, wc, y)
         else:
@@ -184,7 +227,10 @@ class TokenLinear(torch.autograd.Function):
             # that cannot be viewed 2-D (the decoder's [nq, bs, C] transposes)
             # dispatches a bmm against the weight expanded to [nq, C, C]
             x2 = xc.reshape(-1, xc.shape[-1])
-            y2 = torch.mm(x2, wc.t()) if bc is None else torch.addmm(bc, x2, wc.t())
+            if tlin_ok(x2, wc, bc):
+                y2 = tlin_forward(x2, wc, bc)
+            else:
+                y2 = torch.mm(x2, wc.t()) if bc is None else torch.addmm(bc, x2, wc.t())
             y = y2.view(*xc.shape[:-1], wc.shape[0])
             ctx.save_for_backward(xc, wc)
         ctx.relu = relu

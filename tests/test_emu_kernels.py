@@ -1068,3 +1068,31 @@ def test_emulated_query_anchors(transposed, monkeypatch):
     assert ri.shape == ri0.shape == (37, 2, 4, 4) and se.shape == se0.shape == (37, 2, 512)
     assert torch.equal(ri, ri0)
     assert float((se - se0).abs().max()) < 2e-6
+
+
+@pytest.mark.parametrize("m,k,n,relu,bias,pad", [
+    (300, 256, 256, False, True, 0),     # the encoder's 256 -> 256 (tail tile of 44 rows)
+    (257, 96, 288, True, True, 0),       # Swin-T stage 0: K = 96 (half chunk), N = 288 (partial N tile)
+    (130, 384, 96, False, False, 8),     # no bias, x rows padded (ldx = K + 8)
+    (64, 2048, 136, True, True, 0),      # long K, N = 136 (one full and one 8-wide N tile)
+])
+def test_emulated_token_linear_forward(m, k, n, relu, bias, pad):
+    """csrc/tlin.hip y = x W^T (+ b) (ReLU), bf16 in / out, fp32 accumulate,
+    against the fp64 product rounded once to bf16: every element within one
+    bf16 ulp (the accumulation order differs), tails in M, N and K
+    zero-filled and masked."""
+    from emu_product import emulated_product
+    from gdino_amd.wgrad import tlin_forward
+    g = torch.Generator().manual_seed(m + k + n)
+    xs = torch.randn(m, k + pad, generator=g).to(torch.bfloat16)
+    x = xs[:, :k]
+    w = (torch.randn(n, k, generator=g) * k ** -0.5).to(torch.bfloat16)
+    b = torch.randn(n, generator=g).to(torch.bfloat16) if bias else None
+    with emulated_product():
+        y = tlin_forward(x, w, b, relu)
+    ref = x.double() @ w.double().t() + (b.double() if bias else 0)
+    if relu:
+        ref = ref.clamp_min(0)
+    assert y.shape == (m, n) and y.dtype == torch.bfloat16
+    ulp = ref.abs().clamp_min(1e-3) * 2 ** -7
+    assert bool(((y.double() - ref).abs() <= ulp).all()), float(((y.double() - ref).abs() / ulp).max())
