@@ -16,7 +16,8 @@
 // cache lines) into registers, stored to an LDS stage (row pitch 72
 // elements: 16 consecutive rows' 16-B fragment reads hit 64 distinct banks),
 // and the next chunk's loads are in flight while this one is multiplied
-// (two stages).  Fragments are natural-order rows (mfma_frag.inc: lane
+// (two stages; deeper register prefetch and a transposed accumulator layout
+// with 8-B epilogue writes were both measured slower).  Fragments are natural-order rows (mfma_frag.inc: lane
 // (c, g) holds k = 8g..8g+7 of row c), no transposes: both operands are
 // K-contiguous.  Epilogue: + bias, ReLU, bf16, staged through LDS so that
 // each output row leaves as 16-B stores.  Rows >= M, outputs >= N and
@@ -55,32 +56,29 @@ tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __r
   const int L = tl_xcd_logical(int(blockIdx.x), int(gridDim.x));
   const int m0 = (L / tiles_n) * kTlM, n0 = (L % tiles_n) * kTlN;
 
-  // loader: vector v = tid + 256 h (h < 4) of a [128 rows][8 x 16 B] chunk;
-  // two chunks in registers (P = 0 / 1): chunk kc + 2 is loading while
-  // chunk kc + 1 waits in registers and chunk kc is multiplied
+  // loader: vector v = tid + 256 h (h < 4) of a [128 rows][8 x 16 B] chunk
+  // (one chunk in registers: a second set -- 148 VGPRs -- measured slower)
   const int lpart = tid & 7, lrow = tid >> 3;  // rows lrow + 32 h
-  uint4 rx[2][4], rw[2][4];
-  auto load = [&](int p, int k0) {
+  uint4 rx[4], rw[4];
+  auto load = [&](int k0) {
     const int k = k0 + 8 * lpart;
     const bool kok = k < K;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       const int r = lrow + 32 * h;
       const int mr = m0 + r, nr = n0 + r;
-      rx[p][h] = (kok && mr < M) ? *reinterpret_cast<const uint4*>(x + int64_t(mr) * ldx + k)
-                                 : make_uint4(0, 0, 0, 0);
-      rw[p][h] = (kok && nr < N) ? *reinterpret_cast<const uint4*>(w + int64_t(nr) * K + k)
-                                 : make_uint4(0, 0, 0, 0);
+      rx[h] = (kok && mr < M) ? *reinterpret_cast<const uint4*>(x + int64_t(mr) * ldx + k) : make_uint4(0, 0, 0, 0);
+      rw[h] = (kok && nr < N) ? *reinterpret_cast<const uint4*>(w + int64_t(nr) * K + k) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto stash = [&](int p, int buf) {
+  auto stash = [&](int buf) {
     uint16_t* xs = lds + buf * kTlStage;
     uint16_t* ws = xs + kTlM * kTlPitch;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       const int r = lrow + 32 * h;
-      *reinterpret_cast<uint4*>(xs + r * kTlPitch + 8 * lpart) = rx[p][h];
-      *reinterpret_cast<uint4*>(ws + r * kTlPitch + 8 * lpart) = rw[p][h];
+      *reinterpret_cast<uint4*>(xs + r * kTlPitch + 8 * lpart) = rx[h];
+      *reinterpret_cast<uint4*>(ws + r * kTlPitch + 8 * lpart) = rw[h];
     }
   };
 
@@ -91,18 +89,10 @@ tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __r
     for (int j = 0; j < 4; ++j) acc[i][j] = zero4();
 
   const int nchunks = (K + kTlK - 1) / kTlK;
-  load(0, 0);
-  if (nchunks > 1) load(1, kTlK);
+  load(0);
   for (int kc = 0, buf = 0; kc < nchunks; ++kc, buf ^= 1) {
-    // (register sets alternate with kc; the compiler keeps the unrolled
-    // pair's indices static)
-    if (kc & 1) {
-      stash(1, buf);
-      if (kc + 2 < nchunks) load(1, (kc + 2) * kTlK);
-    } else {
-      stash(0, buf);
-      if (kc + 2 < nchunks) load(0, (kc + 2) * kTlK);
-    }
+    stash(buf);
+    if (kc + 1 < nchunks) load((kc + 1) * kTlK);  // next chunk in flight during the MFMAs
     __syncthreads();
     const uint16_t* xs = lds + buf * kTlStage;
     const uint16_t* ws = xs + kTlM * kTlPitch;
