@@ -1,6 +1,6 @@
 """Which part of the whole-step graph refuses HIP-graph capture?
 
-    python tools/capture_probe.py
+    python tools/probes/capture_probe.py
 
 1. One eager train step under torch.cuda.set_sync_debug_mode("warn"): every
    host-synchronising op (the usual capture breakers) is reported with its
@@ -16,7 +16,7 @@ import contextlib
 import sys
 import traceback
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
 import torch  # noqa: E402

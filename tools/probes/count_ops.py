@@ -5,7 +5,7 @@ excluded from the count, each counts as one launch as on the GPU).
 The count does not depend on the image size, so a small image gives the same
 per-step launch profile as 800x1333.  CPU autocast (bf16) approximates CUDA
 autocast's cast insertion.  Usage:
-    python tools/count_ops.py [--top 40] [--no-autocast]
+    python tools/probes/count_ops.py [--top 40] [--no-autocast]
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import collections
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd"), os.path.join(ROOT, "tests")]
 
 import torch  # noqa: E402

@@ -3,7 +3,7 @@ and dump its node list (hipGraphDebugDotPrint through CUDAGraph.debug_dump):
 node types (kernel / memcpy / memset / host / event), copy directions and
 sizes -- the nodes a replay executes that the eager warm-ups did not show.
 
-    python tools/graph_dump.py [--full] [--out gpurun_out/graph.dot]
+    python tools/probes/graph_dump.py [--full] [--out gpurun_out/graph.dot]
 """
 import argparse
 import collections
@@ -12,7 +12,7 @@ import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
 import torch  # noqa: E402

@@ -12,7 +12,7 @@ A long GEMM precedes each probe so that the node before the memset / memcpy
 is still running when the next node could start.  No index is derived from
 the probed data: a reordering shows as a nonzero count, never as a fault.
 
-    python tools/graph_node_order_probe.py [--replays 300] [--mb 64]
+    python tools/probes/graph_node_order_probe.py [--replays 300] [--mb 64]
 """
 import argparse
 import ctypes
@@ -22,7 +22,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
 

@@ -3,12 +3,12 @@ contiguous tensor into a contiguous one of the same dtype on the same device
 with hipMemcpyAsync (a memcpy node when captured); every other copy is a
 kernel.  On ROCm 7.0 eager hipMemcpyAsync calls issued between graph replays
 corrupt the next replay when the graph holds memcpy nodes
-(tools/stepgraph_diag.py --flows: 200 eager D2D copies between two replays
+(tools/probes/stepgraph_diag.py --flows: 200 eager D2D copies between two replays
 change two decoder bias gradients; kernel copies do not), so the step graph
 must hold none.  Logs every such copy of one eager step body, with its size
 and the site (innermost package frame, or the autograd node).
 
-    python tools/memcpy_census.py [--full]
+    python tools/probes/memcpy_census.py [--full]
 """
 import argparse
 import collections
@@ -16,7 +16,7 @@ import os
 import sys
 import traceback
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "open-groundingdino_amd")]
 
 import torch  # noqa: E402

@@ -15,7 +15,7 @@ Sampling locations are the Deformable-DETR initialisation
 (point+1) biases), i.e. exactly the step-0 geometry; during training the
 offsets drift, so the factor is an estimate of the start-of-training case.
 
-    python tools/msda_atomic_study.py
+    python tools/probes/msda_atomic_study.py
 """
 import math
 

@@ -7,7 +7,7 @@ A phase whose host time exceeds its device time starves the GPU (launch
 bound); the criterion's device->host copy for the matching makes the GPU wait
 for the host's LSA and for the first backward launches.
 
-    python tools/step_phases.py [--steps 8] [--warmup 3] [--graphs]
+    python tools/probes/step_phases.py [--steps 8] [--warmup 3] [--graphs]
 """
 from __future__ import annotations
 
@@ -17,7 +17,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "open-groundingdino_amd")]
 
 import torch  # noqa: E402

@@ -2,7 +2,7 @@
 from the eager step's?  The step-graph test's model and batch (lr 0), eager
 vs graph, with pieces of the captured body switched off:
 
-    python tools/stepgraph_diag.py [--clip 0|1] [--opt 0|1] [--full]
+    python tools/probes/stepgraph_diag.py [--clip 0|1] [--opt 0|1] [--full]
 
 Prints the parameters whose replayed gradient differs (relative norm > 1e-3)
 and, for each, the first values of both.
@@ -11,7 +11,7 @@ import argparse
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "open-groundingdino_amd")]
 
 import torch  # noqa: E402
