@@ -221,7 +221,9 @@ class TokenLinear(torch.autograd.Function):
             else:
                 y = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
             y = y.view(*xc.shape[:-1], wc.shape[0])
-            ctx.save_for_backward(xc, wc, y)
+            # x2: the rows the weight gradient reads (already copied once
+            # when xc could not be viewed 2-D -- not again in the backward)
+            ctx.save_for_backward(x2, wc, y)
         else:
             # one 2-D GEMM over the flattened tokens: F.linear on a 3-D input
             # that cannot be viewed 2-D (the decoder's [nq, bs, C] transposes)
@@ -232,7 +234,7 @@ class TokenLinear(torch.autograd.Function):
             else:
                 y2 = torch.mm(x2, wc.t()) if bc is None else torch.addmm(bc, x2, wc.t())
             y = y2.view(*xc.shape[:-1], wc.shape[0])
-            ctx.save_for_backward(xc, wc)
+            ctx.save_for_backward(x2, wc)
         ctx.relu = relu
         ctx.lib_wgrad = lib_wgrad
         ctx.x_dtype = x.dtype
@@ -244,15 +246,16 @@ class TokenLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if ctx.relu:
-            xc, wc, y = ctx.saved_tensors
+            x2, wc, y = ctx.saved_tensors
             dy = torch.ops.aten.threshold_backward(dy.to(wc.dtype), y, 0)
         else:
-            xc, wc = ctx.saved_tensors
+            x2, wc = ctx.saved_tensors
         dy = dy.to(wc.dtype)
-        dx = _dx(dy, wc, ctx.x_dtype) if ctx.needs_input_grad[0] else None
-        i = xc.shape[-1]
+        # one row-major copy of dy at most, shared by dX and dW
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dx = _dx(dy2, wc, ctx.x_dtype).view(*dy.shape[:-1], wc.shape[1]) if ctx.needs_input_grad[0] else None
         wg = weight_grad_lib if ctx.lib_wgrad else weight_grad
-        dw, db = wg(dy.reshape(-1, dy.shape[-1]).contiguous(), xc.reshape(-1, i).contiguous(), ctx.has_bias)
+        dw, db = wg(dy2, x2.contiguous(), ctx.has_bias)
         grads = list(dw.split(ctx.rows, 0))
         if ctx.has_bias:
             grads += list(db.split(ctx.rows, 0))
