@@ -96,7 +96,8 @@ gd_status softmax_fwd(const void* s, const uint8_t* pad_v, const uint8_t* pad_l,
   GD_LAUNCH_CHECK("biattn colmerge");
   const bool contig = contig_ok(Tn, sizeof(T), {s, pv, pl}) && aligned_to(col_m, 16) && aligned_to(col_inv, 16);
   with_slots(Tn, contig, [&](auto e, auto c) {
-    hipLaunchKernelGGL((rows_fwd_kernel<T, decltype(e)::value, decltype(c)::value>), dim3(rblocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((rows_fwd_kernel<T, decltype(e)::value, decltype(c)::value>),
+                       dim3(unsigned((nrows + 4 * kRowsPerWave - 1) / (4 * kRowsPerWave))), dim3(256), 0, st,
                      (const T*)s, pad_v, pad_l, col_m, col_inv, H, S, Tn, nrows, (T*)pv, (T*)pl);
   });
   GD_LAUNCH_CHECK("biattn rows_fwd");
