@@ -422,6 +422,15 @@ gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_
                                     const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,
                                     float* grad_weight, float* grad_bias, void* workspace,
                                     gd_stream_t stream);
+/* The same with grad_y2 (optional, fp32 [rows, C]): the gradient of a second
+ * consumer of y, summed with grad_y inside the kernel (the accumulation add
+ * autograd would run for an output read by two layers).  Python:
+ * gdino_amd.layernorm.add_norm(..., taps=2). */
+gd_status gd_add_layernorm_backward2(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                     const float* weight, const float* grad_y, const float* grad_y2,
+                                     const float* mean, const float* rstd, int64_t rows, int C, void* grad_x,
+                                     void* grad_r, float* grad_weight, float* grad_bias, void* workspace,
+                                     gd_stream_t stream);
 
 /* Three-input add + LayerNorm of the deformable layers' attention sublayer,
  * C = 256: y = LayerNorm(x + (r + dropout(r2))) -- x the fp32 residual
@@ -433,13 +442,16 @@ gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_
  * regenerates the mask.  Backward: grad_x = the gradient of x and of r (the
  * same values), grad_r2 (bf16, optional) = bf16(bf16(ds) / (1 - p)) where
  * kept; grad_weight / grad_bias fp32 (workspace:
- * gd_add_layernorm_workspace_bytes(256)).  Python: gdino_amd.layernorm.add_norm3. */
+ * gd_add_layernorm_workspace_bytes(256)).  grad_y2 (optional): the gradient of a
+ * second consumer of y, summed in the kernel.  Python:
+ * gdino_amd.layernorm.add_norm3. */
 gd_status gd_add_layernorm3_forward(const float* x, const float* r, const void* r2_bf16, const float* weight,
                                     const float* bias, int64_t rows, int C, float eps, float drop_p, uint32_t seed,
                                     const uint32_t* seed_dev, float* y, void* y_bf16, float* mean, float* rstd,
                                     gd_stream_t stream);
 gd_status gd_add_layernorm3_backward(const float* x, const float* r, const void* r2_bf16, const float* weight,
-                                     const float* grad_y, const float* mean, const float* rstd, int64_t rows, int C,
+                                     const float* grad_y, const float* grad_y2, const float* mean, const float* rstd,
+                                     int64_t rows, int C,
                                      float drop_p, uint32_t seed, const uint32_t* seed_dev, float* grad_x,
                                      void* grad_r2_bf16, float* grad_weight, float* grad_bias, void* workspace,
                                      gd_stream_t stream);

@@ -90,10 +90,13 @@ addln_fwd_kernel(const TX* __restrict__ x, const TR* __restrict__ r, const float
   }
 }
 
-// dy [rows, C] fp32 -> dx (TX), dr (TR, optional), partial dw / db per wave
+// dy [rows, C] fp32 (+ dy2, the gradient of a second consumer of y, summed
+// here instead of by an autograd add) -> dx (TX), dr (TR, optional),
+// partial dw / db per wave
 template <typename TX, typename TR, int C>
 __global__ void __launch_bounds__(256)
-addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const TR* __restrict__ r,
+addln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ dy2, const TX* __restrict__ x,
+                 const TR* __restrict__ r,
                  const float* __restrict__ w, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                  int64_t rows, TX* __restrict__ dx, TR* __restrict__ dr, float* __restrict__ part_w,
                  float* __restrict__ part_b) {
@@ -117,7 +120,7 @@ addln_bwd_kernel(const float* __restrict__ dy, const TX* __restrict__ x, const T
       const bool ok = col_ok<C>(lane, e);
       const float s = ok ? ldv<TX>(x + o) + (r ? ldv<TR>(r + o) : 0.f) : 0.f;
       xh[e] = ok ? (s - mean) * rstd : 0.f;
-      const float d = ok ? dy[o] : 0.f;
+      const float d = ok ? dy[o] + (dy2 ? dy2[o] : 0.f) : 0.f;  // dy2: a second consumer's gradient
       gw[e] += d * xh[e];
       gb[e] += d;
       g[e] = d * wv[e];
@@ -285,7 +288,8 @@ addln3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ r, cons
 
 template <int C, bool DROP>
 __global__ void __launch_bounds__(256)
-addln3_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ r,
+addln3_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ dy2, const float* __restrict__ x,
+                  const float* __restrict__ r,
                   const uint16_t* __restrict__ r2, const float* __restrict__ w, const float* __restrict__ mean_in,
                   const float* __restrict__ rstd_in, int64_t rows, Drop3 d, float* __restrict__ dx,
                   uint16_t* __restrict__ dr2, float* __restrict__ part_w, float* __restrict__ part_b) {
@@ -308,7 +312,7 @@ addln3_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x, con
       const int64_t o = row * C + lane + 64 * e;
       const float s = x[o] + (branch3<DROP>(r2, o, uint32_t(row), lane + 64 * e, d) + r[o]);
       xh[e] = (s - mean) * rstd;
-      const float dv = dy[o];
+      const float dv = dy[o] + (dy2 ? dy2[o] : 0.f);
       gw[e] += dv * xh[e];
       gb[e] += dv;
       g[e] = dv * wv[e];
@@ -558,11 +562,26 @@ extern "C" gd_status gd_add_layernorm_forward2(gd_dtype x_dtype, const void* x, 
   return GD_OK;
 }
 
+extern "C" gd_status gd_add_layernorm_backward2(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                               const float* weight, const float* grad_y, const float* grad_y2,
+                                               const float* mean, const float* rstd, int64_t rows, int C,
+                                               void* grad_x, void* grad_r, float* grad_weight, float* grad_bias,
+                                               void* workspace, gd_stream_t stream);
+
 extern "C" gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
                                               const float* weight, const float* grad_y, const float* mean,
                                               const float* rstd, int64_t rows, int C, void* grad_x, void* grad_r,
                                               float* grad_weight, float* grad_bias, void* workspace,
                                               gd_stream_t stream) {
+  return gd_add_layernorm_backward2(x_dtype, x, r_dtype, r, weight, grad_y, nullptr, mean, rstd, rows, C, grad_x,
+                                    grad_r, grad_weight, grad_bias, workspace, stream);
+}
+
+extern "C" gd_status gd_add_layernorm_backward2(gd_dtype x_dtype, const void* x, gd_dtype r_dtype, const void* r,
+                                               const float* weight, const float* grad_y, const float* grad_y2,
+                                               const float* mean, const float* rstd, int64_t rows, int C,
+                                               void* grad_x, void* grad_r, float* grad_weight, float* grad_bias,
+                                               void* workspace, gd_stream_t stream) {
   GD_REQUIRE(rows >= 0, "add_layernorm: rows < 0");
   GD_REQUIRE((grad_weight == nullptr) == (grad_bias == nullptr),
              "add_layernorm_backward: grad_weight and grad_bias are requested together");
@@ -582,7 +601,7 @@ extern "C" gd_status gd_add_layernorm_backward(gd_dtype x_dtype, const void* x, 
     using TX = decltype(tx);
     using TR = decltype(tr);
     hipLaunchKernelGGL((addln_bwd_kernel<TX, TR, decltype(e)::value>), dim3(kLnBlocks), dim3(256), 0, s, grad_y,
-                       (const TX*)x, (const TR*)r, weight, mean, rstd, rows, (TX*)grad_x, (TR*)grad_r, part_w,
+                       grad_y2, (const TX*)x, (const TR*)r, weight, mean, rstd, rows, (TX*)grad_x, (TR*)grad_r, part_w,
                        part_b);
   });
   if (st != GD_OK) return st;
@@ -618,7 +637,8 @@ extern "C" gd_status gd_add_layernorm3_forward(const float* x, const float* r, c
 }
 
 extern "C" gd_status gd_add_layernorm3_backward(const float* x, const float* r, const void* r2_bf16,
-                                               const float* weight, const float* grad_y, const float* mean,
+                                               const float* weight, const float* grad_y, const float* grad_y2,
+                                               const float* mean,
                                                const float* rstd, int64_t rows, int C, float drop_p, uint32_t seed,
                                                const uint32_t* seed_dev, float* grad_x, void* grad_r2_bf16,
                                                float* grad_weight, float* grad_bias, void* workspace,
@@ -638,11 +658,11 @@ extern "C" gd_status gd_add_layernorm3_backward(const float* x, const float* r, 
   float* part_b = part_w + int64_t(kLnBlocks) * C;
   const Drop3 d = make_drop3(drop_p, seed, seed_dev);
   if (drop_p > 0.f)
-    hipLaunchKernelGGL((addln3_bwd_kernel<256, true>), dim3(kLnBlocks), dim3(256), 0, s, grad_y, x, r,
+    hipLaunchKernelGGL((addln3_bwd_kernel<256, true>), dim3(kLnBlocks), dim3(256), 0, s, grad_y, grad_y2, x, r,
                        (const uint16_t*)r2_bf16, weight, mean, rstd, rows, d, grad_x, (uint16_t*)grad_r2_bf16,
                        part_w, part_b);
   else
-    hipLaunchKernelGGL((addln3_bwd_kernel<256, false>), dim3(kLnBlocks), dim3(256), 0, s, grad_y, x, r,
+    hipLaunchKernelGGL((addln3_bwd_kernel<256, false>), dim3(kLnBlocks), dim3(256), 0, s, grad_y, grad_y2, x, r,
                        (const uint16_t*)r2_bf16, weight, mean, rstd, rows, d, grad_x, (uint16_t*)grad_r2_bf16,
                        part_w, part_b);
   GD_LAUNCH_CHECK("add_layernorm3_bwd");

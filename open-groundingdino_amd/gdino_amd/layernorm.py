@@ -35,6 +35,7 @@ def _bf16_twin_wanted(x, wanted: bool = True) -> bool:
 
 TWIN = True
 _lib.register("gd_add_layernorm_backward", [_i, _p, _i, _p, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p])
+_lib.register("gd_add_layernorm_backward2", [_i, _p, _i, _p, _p, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p])
 
 WIDTHS = (64, 96, 128, 192, 256, 384, 512, 768, 1024, 1536, 2048)
 ENABLED = True
@@ -55,9 +56,23 @@ def _workspace(c, device):
     return torch.empty((int(fn(c)) + 3) // 4, dtype=torch.float32, device=device)
 
 
+def _with_taps(y, y16, taps):
+    """y, or (y, a view of y) for an output read by two consumers: autograd
+    then hands the two gradients to the backward separately, whose kernel
+    sums them (no accumulation add).  Both carry the bf16 twin."""
+    if y16 is not None:
+        y._gd_bf16 = (y16, y._version)  # stale once y is modified in place
+    if taps == 1:
+        return y
+    t = y.view(y.shape)
+    if y16 is not None:
+        t._gd_bf16 = (y16, t._version)
+    return y, t
+
+
 class AddLayerNormFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r, weight, bias, eps, twin=True):
+    def forward(ctx, x, r, weight, bias, eps, twin=True, taps=1):
         c = x.shape[-1]
         rows = x.numel() // c
         y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
@@ -70,37 +85,38 @@ class AddLayerNormFunction(torch.autograd.Function):
                   mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(x),
                   nbytes=rows * (c * (x.element_size() + (0 if r is None else r.element_size()) + 4
                                       + (0 if y16 is None else 2)) + 8))
-        if y16 is not None:
-            y._gd_bf16 = (y16, y._version)  # stale once y is modified in place
         ctx.save_for_backward(x, r, weight, mean, rstd)
-        return y
+        return _with_taps(y, y16, taps)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy2=None):
         x, r, weight, mean, rstd = ctx.saved_tensors
         c = x.shape[-1]
         rows = x.numel() // c
+        if dy is None:
+            dy, dy2 = dy2, None
         dy = dy.float().contiguous()
+        dy2 = None if dy2 is None else dy2.float().contiguous()
         dx = torch.empty_like(x)
         dr = torch.empty_like(r) if r is not None and ctx.needs_input_grad[1] else None
         want_wb = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         dw = torch.empty(c, dtype=torch.float32, device=x.device) if want_wb else None
         db = torch.empty(c, dtype=torch.float32, device=x.device) if want_wb else None
         ws = _workspace(c, x.device) if want_wb else None
-        _lib.call("gd_add_layernorm_backward", _lib.dtype_code(x), x.data_ptr(), _lib.dtype_code(x if r is None else r),
-                  _lib.ptr(r),
-                  weight.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, c, dx.data_ptr(),
+        _lib.call("gd_add_layernorm_backward2", _lib.dtype_code(x), x.data_ptr(),
+                  _lib.dtype_code(x if r is None else r), _lib.ptr(r), weight.data_ptr(), dy.data_ptr(), _lib.ptr(dy2),
+                  mean.data_ptr(), rstd.data_ptr(), rows, c, dx.data_ptr(),
                   _lib.ptr(dr), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws), _lib.stream_of(x),
                   nbytes=rows * (c * (2 * x.element_size() + (0 if r is None else r.element_size()) + 4
                                       + (r.element_size() if dr is not None else 0)) + 8))
         return (dx if ctx.needs_input_grad[0] else None, dr, dw if ctx.needs_input_grad[2] else None,
-                db if ctx.needs_input_grad[3] else None, None, None)
+                db if ctx.needs_input_grad[3] else None, None, None, None)
 
 
 _u32 = ctypes.c_uint32
 _lib.register("gd_add_layernorm3_forward", [_p, _p, _p, _p, _p, _i64, _i, _f, _f, _u32, _p, _p, _p, _p, _p, _p])
-_lib.register("gd_add_layernorm3_backward", [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _u32, _p, _p, _p, _p, _p,
-                                              _p, _p])
+_lib.register("gd_add_layernorm3_backward", [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _u32, _p, _p, _p, _p,
+                                              _p, _p, _p])
 
 
 class AddLayerNorm3Function(torch.autograd.Function):
@@ -110,7 +126,7 @@ class AddLayerNorm3Function(torch.autograd.Function):
     replay); the backward regenerates the mask from it."""
 
     @staticmethod
-    def forward(ctx, x, r, r2, weight, bias, eps, p, seed, twin=True):
+    def forward(ctx, x, r, r2, weight, bias, eps, p, seed, twin=True, taps=1):
         rows = x.numel() // 256
         y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         mean = torch.empty(rows, dtype=torch.float32, device=x.device)
@@ -120,41 +136,42 @@ class AddLayerNorm3Function(torch.autograd.Function):
                   bias.data_ptr(), rows, 256, float(eps), float(p), 0, _lib.ptr(seed), y.data_ptr(), _lib.ptr(y16),
                   mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(x),
                   nbytes=rows * (256 * (4 + 4 + 2 + 4 + (0 if y16 is None else 2)) + 8))
-        if y16 is not None:
-            y._gd_bf16 = (y16, y._version)
         ctx.save_for_backward(x, r, r2, weight, mean, rstd, seed)
         ctx.p = float(p)
-        return y
+        return _with_taps(y, y16, taps)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dy2=None):
         x, r, r2, weight, mean, rstd, seed = ctx.saved_tensors
         rows = x.numel() // 256
+        if dy is None:
+            dy, dy2 = dy2, None
         dy = dy.float().contiguous()
+        dy2 = None if dy2 is None else dy2.float().contiguous()
         dx = torch.empty_like(x)
         dr2 = torch.empty_like(r2) if ctx.needs_input_grad[2] else None
         dw = torch.empty(256, dtype=torch.float32, device=x.device)
         db = torch.empty(256, dtype=torch.float32, device=x.device)
         ws = _workspace(256, x.device)
         _lib.call("gd_add_layernorm3_backward", x.data_ptr(), r.data_ptr(), r2.data_ptr(), weight.data_ptr(),
-                  dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, 256, ctx.p, 0, _lib.ptr(seed),
+                  dy.data_ptr(), _lib.ptr(dy2), mean.data_ptr(), rstd.data_ptr(), rows, 256, ctx.p, 0, _lib.ptr(seed),
                   dx.data_ptr(), _lib.ptr(dr2), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), _lib.stream_of(x),
                   nbytes=rows * (256 * (4 + 4 + 4 + 2 + 4 + (2 if dr2 is not None else 0)) + 8))
         # x and r receive the same gradient (one tensor: autograd never
         # accumulates into a gradient it does not own alone)
         return (dx if ctx.needs_input_grad[0] else None, dx if ctx.needs_input_grad[1] else None, dr2,
                 dw if ctx.needs_input_grad[3] else None, db if ctx.needs_input_grad[4] else None, None, None, None,
-                None)
+                None, None)
 
 
 def add_norm3(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, r2: torch.Tensor, dropout: nn.Module,
-              bf16_twin: bool = True) -> torch.Tensor:
+              bf16_twin: bool = True, taps: int = 1):
     """norm(x + (r + dropout(r2))): the deformable layers' attention sublayer
     with the MSDA module's identity add and output dropout folded in (one
     kernel each way instead of dropout, a mixed bf16 + fp32 add and
     add + LayerNorm).  x, r fp32 [..., 256], r2 bf16 of the same shape,
     ``dropout`` an nn.Dropout (its rate and mode) or nn.Identity; None when
-    not applicable (the caller runs the composition)."""
+    not applicable (the caller runs the composition).  taps=2 as in add_norm."""
     p = float(getattr(dropout, "p", 0.0)) if dropout.training else 0.0
     if not (supported(norm, x, r) and x.shape[-1] == 256 and x.dtype == r.dtype == torch.float32
             and r2.dtype == torch.bfloat16 and r2.shape == x.shape and (p == 0.0 or isinstance(dropout, nn.Dropout))
@@ -162,7 +179,7 @@ def add_norm3(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, r2: torch.Te
         return None
     seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=x.device) if p > 0 else None
     return AddLayerNorm3Function.apply(x.contiguous(), r.contiguous(), r2.contiguous(), norm.weight, norm.bias,
-                                       norm.eps, p, seed, bool(bf16_twin))
+                                       norm.eps, p, seed, bool(bf16_twin), int(taps))
 
 
 _lib.register("gd_add_scaled_layernorm_forward", [_p, _i, _p, _p, _i64, _i, _p, _p, _i64, _i, _f, _p, _p, _p, _p,
@@ -254,11 +271,14 @@ def layer_norm(norm: nn.LayerNorm, x: torch.Tensor, bf16_twin: bool = True) -> t
     return norm(x)
 
 
-def add_norm(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, bf16_twin: bool = True) -> torch.Tensor:
-    """norm(x + r); ``bf16_twin`` as in layer_norm"""
+def add_norm(norm: nn.LayerNorm, x: torch.Tensor, r: torch.Tensor, bf16_twin: bool = True, taps: int = 1):
+    """norm(x + r); ``bf16_twin`` as in layer_norm.  taps=2: (y, y') for an
+    output read by two consumers -- hand one to each; their gradients are
+    summed inside the backward kernel."""
     if supported(norm, x, r):
         # (the decoder's MSDA output arrives transposed: one copy, which the
         # unfused add would pay as well)
         return AddLayerNormFunction.apply(x.contiguous(), r.contiguous(), norm.weight, norm.bias, norm.eps,
-                                          bool(bf16_twin))
-    return norm(x + r)
+                                          bool(bf16_twin), int(taps))
+    y = norm(x + r)
+    return y if taps == 1 else (y, y)

@@ -439,9 +439,10 @@ class DeformableTransformerEncoderLayer(nn.Module):
     def with_pos_embed(tensor, pos):
         return tensor if pos is None else tensor + pos
 
-    def forward_ffn(self, src):
+    def forward_ffn(self, src, resid=None):
+        """resid: a second handle on src (add_norm taps) for the residual"""
         src2 = self.linear2(self.dropout2(ffn_act(self.linear1, self.activation, src)))
-        return add_norm(self.norm2, src, self.dropout3(src2))
+        return add_norm(self.norm2, src if resid is None else resid, self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, key_padding_mask=None):
         query = self.with_pos_embed(src, pos)
@@ -452,9 +453,12 @@ class DeformableTransformerEncoderLayer(nn.Module):
             # add + LayerNorm kernel (gdino_amd.layernorm.add_norm3)
             out = msda_attend(sa, query, src, reference_points, spatial_shapes, level_start_index,
                               key_padding_mask, sa.num_heads, sa.num_levels, sa.num_points, sa.im2col_step)
-            y = add_norm3(self.norm1, src, query, out, sa.dropout)
-            src = y if y is not None else add_norm(self.norm1, src, sa.dropout(out) + query)
-            return self.forward_ffn(src)
+            # two handles on the output (FFN input, FFN residual): the two
+            # gradients are summed in the add + LayerNorm backward kernel
+            y = add_norm3(self.norm1, src, query, out, sa.dropout, taps=2)
+            if y is None:
+                y = add_norm(self.norm1, src, sa.dropout(out) + query, taps=2)
+            return self.forward_ffn(*y)
         src2 = sa(query=query, reference_points=reference_points, value=src, spatial_shapes=spatial_shapes,
                   level_start_index=level_start_index, key_padding_mask=key_padding_mask)
         src = add_norm(self.norm1, src, self.dropout1(src2))
@@ -496,12 +500,12 @@ class DeformableTransformerDecoderLayer(nn.Module):
     def with_pos_embed(tensor, pos):
         return tensor if pos is None else tensor + pos
 
-    def forward_ffn(self, tgt):
+    def forward_ffn(self, tgt, resid=None):
         # the reference runs the decoder FFN outside autocast (fp32, :870-875)
         with torch.autocast(device_type=tgt.device.type, enabled=False):
             t = tgt.float() if tgt.dtype in (torch.float16, torch.bfloat16) else tgt
             tgt2 = self.linear2(self.dropout3(ffn_act(self.linear1, self.activation, t)))
-        return add_norm(self.norm3, tgt, self.dropout4(tgt2))
+        return add_norm(self.norm3, tgt if resid is None else resid, self.dropout4(tgt2))
 
     def forward(self, tgt, tgt_query_pos=None, tgt_query_sine_embed=None, tgt_key_padding_mask=None,
                 tgt_reference_points=None, memory_text=None, text_attention_mask=None, memory=None,
@@ -511,16 +515,25 @@ class DeformableTransformerDecoderLayer(nn.Module):
         if self.self_attn is not None:
             q = k = self.with_pos_embed(tgt, tgt_query_pos)
             tgt2 = self.self_attn(q, k, tgt, attn_mask=self_attn_mask)[0]
-            tgt = add_norm(self.norm2, tgt, self.dropout2(tgt2))
+            if self.use_text_cross_attention:
+                # two handles (the text cross-attention's query, its residual)
+                tgt_q, tgt = add_norm(self.norm2, tgt, self.dropout2(tgt2), taps=2)
+            else:
+                tgt = tgt_q = add_norm(self.norm2, tgt, self.dropout2(tgt2))
+        else:
+            tgt_q = tgt
         if self.use_text_cross_attention:
             # key and value are the same tensor (reference :900-905 passes
             # two identical transposes): one object lets the MHA project them
             # with one GEMM
             text_kv = memory_text.transpose(0, 1)
-            tgt2 = self.ca_text(self.with_pos_embed(tgt, tgt_query_pos), text_kv, text_kv,
+            tgt2 = self.ca_text(self.with_pos_embed(tgt_q, tgt_query_pos), text_kv, text_kv,
                                 key_padding_mask=text_attention_mask)[0]
-            tgt = add_norm(self.catext_norm, tgt, self.catext_dropout(tgt2))
-        query = self.with_pos_embed(tgt, tgt_query_pos)
+            # two handles (the deformable attention's query, its residual)
+            tgt_q, tgt = add_norm(self.catext_norm, tgt, self.catext_dropout(tgt2), taps=2)
+        else:
+            tgt_q = tgt
+        query = self.with_pos_embed(tgt_q, tgt_query_pos)
         ca = self.cross_attn
         ref_t = tgt_reference_points.transpose(0, 1).contiguous()
         if ca.identity_add and ca.batch_first and _inert(self.dropout1):
@@ -529,9 +542,10 @@ class DeformableTransformerDecoderLayer(nn.Module):
             out = msda_attend(ca, query.transpose(0, 1), memory.transpose(0, 1), ref_t, memory_spatial_shapes,
                               memory_level_start_index, memory_key_padding_mask, ca.num_heads, ca.num_levels,
                               ca.num_points, ca.im2col_step).transpose(0, 1)
-            y = add_norm3(self.norm1, tgt, query, out, ca.dropout)
-            tgt = y if y is not None else add_norm(self.norm1, tgt, ca.dropout(out) + query)
-            return self.forward_ffn(tgt)
+            y = add_norm3(self.norm1, tgt, query, out, ca.dropout, taps=2)
+            if y is None:
+                y = add_norm(self.norm1, tgt, ca.dropout(out) + query, taps=2)
+            return self.forward_ffn(*y)
         tgt2 = ca(query=query.transpose(0, 1), reference_points=ref_t, value=memory.transpose(0, 1),
                   spatial_shapes=memory_spatial_shapes, level_start_index=memory_level_start_index,
                   key_padding_mask=memory_key_padding_mask).transpose(0, 1)

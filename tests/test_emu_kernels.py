@@ -1096,3 +1096,36 @@ def test_emulated_token_linear_forward(m, k, n, relu, bias, pad):
     assert y.shape == (m, n) and y.dtype == torch.bfloat16
     ulp = ref.abs().clamp_min(1e-3) * 2 ** -7
     assert bool(((y.double() - ref).abs() <= ulp).all()), float(((y.double() - ref).abs() / ulp).max())
+
+
+@pytest.mark.parametrize("three", [False, True])
+def test_emulated_add_norm_two_handles(three):
+    """add_norm / add_norm3 with taps=2: two handles on the output, each read
+    by its own consumer; the backward kernel sums their gradients (no
+    autograd accumulation add) -- same gradients as one output read twice."""
+    from emu_product import emulated_product
+    from gdino_amd.layernorm import add_norm, add_norm3
+    g = torch.Generator().manual_seed(9)
+    norm = torch.nn.LayerNorm(256)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(256, generator=g))
+        norm.bias.copy_(torch.randn(256, generator=g))
+    x0, r0 = torch.randn(3, 40, 256, generator=g), torch.randn(3, 40, 256, generator=g)
+    r20 = torch.randn(3, 40, 256, generator=g).to(torch.bfloat16)
+    ga, gb = torch.randn(3, 40, 256, generator=g), torch.randn(3, 40, 256, generator=g)
+    out = {}
+    for taps in (1, 2):
+        x, r, r2 = (t.clone().requires_grad_(True) for t in (x0, r0, r20))
+        norm.zero_grad()
+        with emulated_product():
+            if three:
+                y = add_norm3(norm, x, r, r2, torch.nn.Identity(), taps=taps)
+            else:
+                y = add_norm(norm, x, r2, taps=taps)
+            ya, yb = (y, y) if taps == 1 else y
+            assert ya.shape == yb.shape == x.shape
+            ((ya * ga).sum() + (yb.sin() * gb).sum()).backward()
+        out[taps] = [t.grad.clone() for t in ((x, r, r2) if three else (x, r2))] + [norm.weight.grad.clone(),
+                                                                                     norm.bias.grad.clone()]
+    for a, b in zip(out[2], out[1]):
+        assert E.rel_err(a.float(), b.float()) < (1e-2 if a.dtype == torch.bfloat16 else 1e-6)
