@@ -597,6 +597,14 @@ gd_status gd_device_status(gd_stream_t stream);
  * Python: gdino_amd.wgrad.TokenLinear. */
 gd_status gd_token_linear_forward(const void* x, int64_t ldx, const void* weight, const void* bias, int M, int K,
                                   int N, int relu, void* y, int64_t ldy, gd_stream_t stream);
+/* The same product with the backward of a ReLU folded into the store:
+ * y = (x . W^T) where mask[M, N] > 0, else 0 (mask rows ldm apart, bf16) --
+ * the input gradient of the FFN's second Linear, whose input is the first
+ * Linear's ReLU output (reference transformer.py:784-790 forward_ffn:
+ * linear2(dropout(relu(linear1(src))))), so the ReLU's threshold pass over
+ * the [tokens, d_ffn] gradient is gone.  Python: gdino_amd.wgrad.TokenLinear. */
+gd_status gd_token_linear_forward_masked(const void* x, int64_t ldx, const void* weight, int M, int K, int N,
+                                         const void* mask, int64_t ldm, void* y, int64_t ldy, gd_stream_t stream);
 /* ABI version: bumped when a signature changes. */
 int gd_abi_version(void);
 

@@ -44,11 +44,23 @@ __device__ __forceinline__ int tl_xcd_logical(int h, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + h / 8;
 }
 
-template <bool RELU, bool BIAS>
+// the two bf16 halves of o where the matching half of m is > 0 (else +0):
+// threshold_backward(o, m, 0) on a pair
+__device__ __forceinline__ uint32_t tl_keep2(uint32_t o, uint32_t m) {
+  const uint32_t lo = __uint_as_float(m << 16) > 0.f ? 0x0000ffffu : 0u;
+  const uint32_t hi = __uint_as_float(m & 0xffff0000u) > 0.f ? 0xffff0000u : 0u;
+  return o & (lo | hi);
+}
+
+// MASK: y = (x . w^T) where mask > 0, else 0 -- the input gradient of a
+// Linear whose input was a ReLU output (mask), with the ReLU's backward folded
+// into the store (applied after the bf16 rounding, as threshold_backward on
+// the bf16 product would)
+template <bool RELU, bool BIAS, bool MASK>
 __global__ void __launch_bounds__(256)
 tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ w,
                 const uint16_t* __restrict__ bias, int M, int K, int N, uint16_t* __restrict__ y, int64_t ldy,
-                int tiles_n) {
+                int tiles_n, const uint16_t* __restrict__ mask, int64_t ldm) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kTlStage];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -81,6 +93,21 @@ tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __r
       *reinterpret_cast<uint4*>(ws + r * kTlPitch + 8 * lpart) = rw[h];
     }
   };
+
+  // MASK: this thread's 8 mask vectors (the epilogue's store mapping) are
+  // loaded up front, their latency hidden behind the K loop (the VGPRs are
+  // free: LDS already limits the CU to two workgroups; loaded after the
+  // loop they cost 70 us of the 165 at the encoder FFN shape)
+  uint4 mreg[MASK ? 8 : 1];
+  if (MASK) {
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const int v = tid + 256 * h;
+      const int mr = m0 + (v >> 4), col = n0 + 8 * (v & 15);
+      mreg[h] = (mr < M && col < N) ? *reinterpret_cast<const uint4*>(mask + int64_t(mr) * ldm + col)
+                                    : make_uint4(0, 0, 0, 0);
+    }
+  }
 
   gd_f32x4 acc[4][4];
 #pragma unroll
@@ -136,9 +163,17 @@ tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __r
     const int v = tid + 256 * h;
     const int row = v >> 4, part = v & 15;
     const int mr = m0 + row, col = n0 + 8 * part;
-    if (mr < M && col < N)
-      *reinterpret_cast<uint4*>(y + int64_t(mr) * ldy + col) =
-          *reinterpret_cast<const uint4*>(ot + row * kTlOutPitch + 8 * part);
+    if (mr < M && col < N) {
+      uint4 o = *reinterpret_cast<const uint4*>(ot + row * kTlOutPitch + 8 * part);
+      if (MASK) {
+        const uint4 mv = mreg[h];
+        o.x = tl_keep2(o.x, mv.x);
+        o.y = tl_keep2(o.y, mv.y);
+        o.z = tl_keep2(o.z, mv.z);
+        o.w = tl_keep2(o.w, mv.w);
+      }
+      *reinterpret_cast<uint4*>(y + int64_t(mr) * ldy + col) = o;
+    }
   }
 }
 
@@ -169,19 +204,40 @@ extern "C" gd_status gd_token_linear_forward(const void* x, int64_t ldx, const v
   uint16_t* yp = static_cast<uint16_t*>(y);
   if (relu) {
     if (bias)
-      hipLaunchKernelGGL((tlin_fwd_kernel<true, true>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
-                         tiles_n);
+      hipLaunchKernelGGL((tlin_fwd_kernel<true, true, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp,
+                         ldy, tiles_n, nullptr, 0);
     else
-      hipLaunchKernelGGL((tlin_fwd_kernel<true, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
-                         tiles_n);
+      hipLaunchKernelGGL((tlin_fwd_kernel<true, false, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp,
+                         ldy, tiles_n, nullptr, 0);
   } else {
     if (bias)
-      hipLaunchKernelGGL((tlin_fwd_kernel<false, true>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
-                         tiles_n);
+      hipLaunchKernelGGL((tlin_fwd_kernel<false, true, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp,
+                         ldy, tiles_n, nullptr, 0);
     else
-      hipLaunchKernelGGL((tlin_fwd_kernel<false, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp, ldy,
-                         tiles_n);
+      hipLaunchKernelGGL((tlin_fwd_kernel<false, false, false>), grid, dim3(256), 0, s, xp, ldx, wp, bp, M, K, N, yp,
+                         ldy, tiles_n, nullptr, 0);
   }
   GD_LAUNCH_CHECK("token_linear_forward");
+  return GD_OK;
+}
+
+extern "C" gd_status gd_token_linear_forward_masked(const void* x, int64_t ldx, const void* weight, int M, int K,
+                                                   int N, const void* mask, int64_t ldm, void* y, int64_t ldy,
+                                                   gd_stream_t stream) {
+  GD_REQUIRE(M >= 0 && K > 0 && N > 0 && K % 8 == 0 && N % 8 == 0,
+             "token_linear_masked: M=%d K=%d N=%d (K, N multiples of 8)", M, K, N);
+  if (M == 0) return GD_OK;
+  GD_REQUIRE(x && weight && mask && y, "token_linear_masked: null pointer");
+  GD_REQUIRE(aligned16(x) && aligned16(weight) && aligned16(mask) && aligned16(y) && ldx % 8 == 0 && ldm % 8 == 0 &&
+                 ldy % 8 == 0 && ldx >= K && ldm >= N && ldy >= N,
+             "token_linear_masked: 16-byte aligned rows required (ldx=%lld ldm=%lld ldy=%lld)", (long long)ldx,
+             (long long)ldm, (long long)ldy);
+  const int tiles_m = (M + kTlM - 1) / kTlM, tiles_n = (N + kTlN - 1) / kTlN;
+  GD_REQUIRE(int64_t(tiles_m) * tiles_n < (int64_t(1) << 31), "token_linear_masked: grid too large");
+  hipLaunchKernelGGL((tlin_fwd_kernel<false, false, true>), dim3(unsigned(tiles_m * tiles_n)), dim3(256), 0,
+                     as_hip(stream), static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(weight),
+                     nullptr, M, K, N, static_cast<uint16_t*>(y), ldy, tiles_n, static_cast<const uint16_t*>(mask),
+                     ldm);
+  GD_LAUNCH_CHECK("token_linear_forward_masked");
   return GD_OK;
 }

@@ -85,6 +85,41 @@ def tlin_forward(x2: torch.Tensor, wc: torch.Tensor, bc=None, relu: bool = False
     return y
 
 
+# the input gradient of a Linear fed by a relu TokenLinear's output, with the
+# ReLU's backward in the store (csrc/tlin.hip MASK): replaces the library dX
+# GEMM + a threshold pass over [tokens, d_ffn] (the encoder FFN: 6 x 546 MB
+# of threshold traffic per step, profiles/r05t_glue_census.txt).
+# GD_TLIN_MASKED=0: the unfused path (A/B)
+_lib.register("gd_token_linear_forward_masked", [_p, _i64, _p, _i, _i, _i, _p, _i64, _p, _i64, _p])
+TLIN_MASKED = os.environ.get("GD_TLIN_MASKED", "1") != "0"
+TLIN_MASKED_MIN_TOKENS = 8192
+
+
+def masked_dx_ok(x: torch.Tensor, wc: torch.Tensor) -> bool:
+    """Route this Linear's dX to gd_token_linear_forward_masked: x is the
+    output of a relu TokenLinear (tagged ``_gd_relu_box``; its only consumer),
+    bf16 contiguous rows, both feature counts multiples of 8, enough tokens."""
+    if not (TLIN_MASKED and TLIN and getattr(x, "_gd_relu_box", None) is not None and _lib.enabled("tlin")
+            and _lib.on_device(x) and x.dtype == wc.dtype == torch.bfloat16 and x.is_contiguous()
+            and wc.is_contiguous() and x.data_ptr() % 16 == 0):
+        return False
+    n_out, k_in = wc.shape
+    return x.numel() // max(k_in, 1) >= TLIN_MASKED_MIN_TOKENS and n_out % 8 == 0 and k_in % 8 == 0
+
+
+def masked_dx(dy2: torch.Tensor, wc: torch.Tensor, mask2: torch.Tensor) -> torch.Tensor:
+    """dX [M, K_in] bf16 = (dy2 [M, N_out] . wc [N_out, K_in]) where
+    mask2 [M, K_in] > 0, else 0."""
+    m, n_out = dy2.shape
+    k_in = wc.shape[1]
+    wt = wc.t().contiguous()  # [K_in, N_out]: the kernel's K-contiguous W
+    y = torch.empty(m, k_in, dtype=torch.bfloat16, device=dy2.device)
+    _lib.call("gd_token_linear_forward_masked", dy2.data_ptr(), dy2.stride(0), wt.data_ptr(), m, n_out, k_in,
+              mask2.data_ptr(), mask2.stride(0), y.data_ptr(), y.stride(0), _lib.stream_of(dy2),
+              flops=2.0 * m * n_out * k_in)
+    return y
+
+
 def eligible(x: torch.Tensor, out_features: int, dtype=None) -> bool:
     """Route a Linear's weight gradient to the split-K kernel: GPU, T >= MIN_TOKENS
     tokens, O and I multiples of 16 (bf16, the 128 x 128 transposed-read
@@ -221,6 +256,10 @@ class TokenLinear(torch.autograd.Function):
             else:
                 y = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
             y = y.view(*xc.shape[:-1], wc.shape[0])
+            # set by the consumer Linear when it folds this ReLU's backward
+            # into its own dX (masked_dx): the gradient arrives masked
+            ctx.relu_box = [False]
+            y._gd_relu_box = ctx.relu_box
             # x2: the rows the weight gradient reads (already copied once
             # when xc could not be viewed 2-D -- not again in the backward)
             ctx.save_for_backward(x2, wc, y)
@@ -235,6 +274,9 @@ class TokenLinear(torch.autograd.Function):
                 y2 = torch.mm(x2, wc.t()) if bc is None else torch.addmm(bc, x2, wc.t())
             y = y2.view(*xc.shape[:-1], wc.shape[0])
             ctx.save_for_backward(x2, wc)
+            ctx.mask_dx = xc is x and masked_dx_ok(x, wc)
+            if ctx.mask_dx:
+                x._gd_relu_box[0] = True
         ctx.relu = relu
         ctx.lib_wgrad = lib_wgrad
         ctx.x_dtype = x.dtype
@@ -247,13 +289,19 @@ class TokenLinear(torch.autograd.Function):
     def backward(ctx, dy):
         if ctx.relu:
             x2, wc, y = ctx.saved_tensors
-            dy = torch.ops.aten.threshold_backward(dy.to(wc.dtype), y, 0)
+            if not ctx.relu_box[0]:  # (else dy was masked by the consumer's dX kernel)
+                dy = torch.ops.aten.threshold_backward(dy.to(wc.dtype), y, 0)
         else:
             x2, wc = ctx.saved_tensors
         dy = dy.to(wc.dtype)
         # one row-major copy of dy at most, shared by dX and dW
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        dx = _dx(dy2, wc, ctx.x_dtype).view(*dy.shape[:-1], wc.shape[1]) if ctx.needs_input_grad[0] else None
+        if not ctx.needs_input_grad[0]:
+            dx = None
+        elif not ctx.relu and ctx.mask_dx:
+            dx = masked_dx(dy2, wc, x2).view(*dy.shape[:-1], wc.shape[1])
+        else:
+            dx = _dx(dy2, wc, ctx.x_dtype).view(*dy.shape[:-1], wc.shape[1])
         wg = weight_grad_lib if ctx.lib_wgrad else weight_grad
         dw, db = wg(dy2, x2.contiguous(), ctx.has_bias)
         grads = list(dw.split(ctx.rows, 0))

@@ -1098,6 +1098,61 @@ def test_emulated_token_linear_forward(m, k, n, relu, bias, pad):
     assert bool(((y.double() - ref).abs() <= ulp).all()), float(((y.double() - ref).abs() / ulp).max())
 
 
+@pytest.mark.parametrize("m,k,n,pad", [(300, 256, 2048, 0), (130, 64, 136, 8)])
+def test_emulated_token_linear_forward_masked(m, k, n, pad):
+    """gd_token_linear_forward_masked: the bf16 product where the mask is
+    > 0, +0 elsewhere (threshold_backward on the rounded product: negative,
+    zero and NaN mask entries all drop the element)."""
+    from emu_product import emulated_product
+    from gdino_amd.wgrad import masked_dx
+    g = torch.Generator().manual_seed(m + n)
+    dys = torch.randn(m, k + pad, generator=g).to(torch.bfloat16)
+    dy = dys[:, :k]
+    w = (torch.randn(k, n, generator=g) * k ** -0.5).to(torch.bfloat16)  # [N_out, K_in] of the Linear
+    mask = torch.randn(m, n, generator=g).clamp_min(0).to(torch.bfloat16)
+    mask[0, :8] = float("nan")
+    mask[1, :8] = -0.0
+    with emulated_product():
+        y = masked_dx(dy, w, mask)
+    ref = dy.double() @ w.double()
+    keep = mask.double() > 0
+    assert y.shape == (m, n) and y.dtype == torch.bfloat16
+    assert bool((y[~keep] == 0).all()) and not bool(torch.signbit(y[~keep]).any())
+    ulp = ref.abs().clamp_min(1e-3) * 2 ** -7
+    assert bool(((y.double() - ref).abs()[keep] <= ulp[keep]).all())
+
+
+def test_emulated_relu_linear_pair_folds_the_threshold(monkeypatch):
+    """relu TokenLinear -> TokenLinear (the FFN): the second Linear's dX
+    kernel applies the ReLU's mask and the first skips its threshold pass;
+    every gradient matches the unfused pair (GD_TLIN_MASKED=0) within the
+    bf16 rounding of dX."""
+    from emu_product import emulated_product
+    from gdino_amd import wgrad
+    monkeypatch.setattr(wgrad, "TLIN_MASKED_MIN_TOKENS", 64)
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.randn(2, 96, 64, generator=g)
+    w1, b1 = torch.randn(128, 64, generator=g) * 0.125, torch.randn(128, generator=g) * 0.1
+    w2, b2 = torch.randn(64, 128, generator=g) * 0.09, torch.randn(64, generator=g) * 0.1
+    gy = torch.randn(2, 96, 64, generator=g)
+
+    def run(fold):
+        monkeypatch.setattr(wgrad, "TLIN_MASKED", fold)
+        x = x0.to(torch.bfloat16).requires_grad_()
+        ps = [t.clone().requires_grad_() for t in (w1, b1, w2, b2)]
+        with emulated_product():
+            h = wgrad.token_linear(x, ps[0].to(torch.bfloat16), ps[1].to(torch.bfloat16), [ps[0]], [ps[1]],
+                                   relu=True)
+            y = wgrad.token_linear(h, ps[2].to(torch.bfloat16), ps[3].to(torch.bfloat16), [ps[2]], [ps[3]])
+            (y.float() * gy).sum().backward()
+        return h._gd_relu_box[0], [x.grad] + [p.grad for p in ps]
+
+    (folded, got), (unfolded, ref) = run(True), run(False)
+    assert folded and not unfolded
+    for a, b in zip(got, ref):
+        assert float((a.float() - b.float()).abs().max()) <= 2e-2 * float(b.float().abs().max())
+
+
 @pytest.mark.parametrize("three", [False, True])
 def test_emulated_add_norm_two_handles(three):
     """add_norm / add_norm3 with taps=2: two handles on the output, each read

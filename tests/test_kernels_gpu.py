@@ -794,3 +794,27 @@ def test_box_refine_matches_composition(dd, monkeypatch):
     assert _rel(got[0], want[0]) < 1e-6
     assert _rel(got[1], want[1]) < (1e-6 if dd == torch.float32 else 2 ** -7)
     assert _rel(got[2], want[2]) < 1e-5
+
+
+@pytest.mark.parametrize("m,k,n", [(44446, 256, 2048), (2048 + 40, 256, 136)])
+def test_token_linear_forward_and_masked_dx(m, k, n):
+    """csrc/tlin.hip at the encoder FFN shape: the relu forward
+    (y = relu(x W1^T + b1)) and the masked input gradient of the second
+    Linear ((dy W2) where y > 0) against fp32 references, bf16 1e-2; the
+    dropped elements are exact +0."""
+    from gdino_amd.wgrad import masked_dx, tlin_forward
+    g = torch.Generator().manual_seed(m)
+    x = torch.randn(m, k, generator=g).to(DEV, torch.bfloat16)
+    w1 = (torch.randn(n, k, generator=g) * k ** -0.5).to(DEV, torch.bfloat16)
+    b1 = torch.randn(n, generator=g).to(DEV, torch.bfloat16)
+    w2 = (torch.randn(k, n, generator=g) * n ** -0.5).to(DEV, torch.bfloat16)
+    y = tlin_forward(x, w1, b1, relu=True)
+    ref = torch.relu(x.float() @ w1.float().t() + b1.float())
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn(m, k, generator=g).to(DEV, torch.bfloat16)
+    dh = masked_dx(dy, w2, y)
+    dref = torch.where(y > 0, dy.float() @ w2.float(), torch.zeros((), device=DEV))
+    torch.cuda.synchronize()
+    assert _rel(dh, dref) < 1e-2
+    drop = ~(y > 0)
+    assert bool((dh[drop] == 0).all()) and not bool(torch.signbit(dh[drop]).any())
