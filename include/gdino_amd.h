@@ -499,6 +499,14 @@ gd_status gd_add_scaled_backward(gd_dtype g_dtype, const void* grad_out, gd_dtyp
                                  const void* branch, const float* s, int64_t s_bstride, int s_cstride,
                                  int64_t B, int64_t N, int C, void* grad_branch, float* grad_s_bc,
                                  void* workspace, gd_stream_t stream);
+/* out[n] = a + b (fp32, n % 4 == 0, 16-B aligned) with the bf16 copies of out
+ * and of a (each optional, NULL) written in the same pass: the encoder's
+ * with_pos_embed (reference transformer.py:780-781, query = src + pos) feeding
+ * the bf16 sampling-offset / attention-weight and value projections
+ * (ms_deform_attn.py:290-297 under autocast).  Python:
+ * gdino_amd.misc.add_with_twins. */
+gd_status gd_add_twin_forward(const float* a, const float* b, int64_t n, float* out, void* out_bf16, void* a_bf16,
+                              gd_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Box refinement: out = sigmoid(delta + inverse_sigmoid(ref))               */

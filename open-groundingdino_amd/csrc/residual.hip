@@ -142,6 +142,25 @@ add_scaled_merge_kernel(const float* __restrict__ part, int chunks, int C, float
   }
 }
 
+// out = a + b (fp32) with the bf16 copies of out and of a written in the
+// same pass (either copy optional): the encoder's query = src + pos, whose
+// two Linears (sampling offsets / attention weights on the query, value_proj
+// on src) read bf16 -- one pass instead of the add and two cast kernels
+__global__ void __launch_bounds__(256)
+add_twin_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t nvec, float* __restrict__ out,
+                uint16_t* __restrict__ out16, uint16_t* __restrict__ a16) {
+  for (int64_t v = int64_t(blockIdx.x) * 256 + threadIdx.x; v < nvec; v += int64_t(gridDim.x) * 256) {
+    const int64_t e = v * 4;
+    const f4 av = ld4<float>(a + e), bv = ld4<float>(b + e);
+    f4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o.v[k] = av.v[k] + bv.v[k];
+    st4<float>(out + e, o);
+    if (out16) st4<uint16_t>(out16 + e, o);
+    if (a16) st4<uint16_t>(a16 + e, av);
+  }
+}
+
 constexpr int kScaledChunks = 256;  // backward chunks per sample (max)
 
 template <typename Fn>
@@ -235,5 +254,19 @@ extern "C" gd_status gd_add_scaled_backward(gd_dtype g_dtype, const void* grad_o
                        int(chunks), C, grad_s_bc);
     GD_LAUNCH_CHECK("add_scaled_merge");
   }
+  return GD_OK;
+}
+
+extern "C" gd_status gd_add_twin_forward(const float* a, const float* b, int64_t n, float* out, void* out_bf16,
+                                        void* a_bf16, gd_stream_t stream) {
+  GD_REQUIRE(n >= 0 && n % 4 == 0, "add_twin: n=%lld (a multiple of 4)", (long long)n);
+  if (n == 0) return GD_OK;
+  GD_REQUIRE(a && b && out, "add_twin: null pointer");
+  const int64_t nvec = n / 4;
+  const int64_t blocks64 = (nvec + 255) / 256;
+  const unsigned blocks = unsigned(blocks64 < 16384 ? blocks64 : 16384);
+  hipLaunchKernelGGL(add_twin_kernel, dim3(blocks), dim3(256), 0, as_hip(stream), a, b, nvec, out,
+                     static_cast<uint16_t*>(out_bf16), static_cast<uint16_t*>(a_bf16));
+  GD_LAUNCH_CHECK("add_twin");
   return GD_OK;
 }

@@ -324,6 +324,47 @@ _lib.register("gd_add_scaled_forward", [_i, _p, _i, _p, _p, _i64, _i, _i64, _i64
 _lib.register("gd_add_scaled_backward", [_i, _p, _i, _p, _p, _i64, _i, _i64, _i64, _i, _p, _p, _p, _p])
 
 
+_lib.register("gd_add_twin_forward", [_p, _p, _i64, _p, _p, _p, _p])
+
+
+class _AddTwins(torch.autograd.Function):
+    """out = a + b (fp32); the same kernel writes the bf16 copies of out and
+    of a into the given buffers (out16, a16: no gradient)."""
+
+    @staticmethod
+    def forward(ctx, a, b, out16, a16):
+        out = torch.empty_like(a)
+        _lib.call("gd_add_twin_forward", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), out16.data_ptr(),
+                  _lib.ptr(a16), _lib.stream_of(a), nbytes=a.numel() * (12 + (2 if a16 is None else 4)))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g, None, None
+
+
+def add_with_twins(a: Tensor, b: Tensor) -> Tensor:
+    """a + b, plus bf16 twins of the sum and of ``a`` written in the same
+    pass when both feed bf16-autocast Linears (the deformable encoder layer's
+    query = src + pos, reference transformer.py:780-781: the query feeds the
+    sampling-offset / attention-weight projections, src the value projection,
+    ms_deform_attn.py:290-297) -- one kernel instead of the add and two cast
+    kernels.  Elsewhere the plain add."""
+    if not (_lib.enabled("addscaled") and _lib.on_device(a) and torch.is_autocast_enabled(a.device.type)
+            and torch.get_autocast_dtype(a.device.type) == torch.bfloat16 and a.dtype == b.dtype == torch.float32
+            and a.shape == b.shape and a.numel() % 4 == 0 and _aligned(a, b)):
+        return a + b
+    tw = getattr(a, "_gd_bf16", None)
+    have_a = tw is not None and tw[1] == a._version and tw[0].dtype == torch.bfloat16 and tw[0].shape == a.shape
+    out16 = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
+    a16 = None if have_a else torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
+    out = _AddTwins.apply(a, b, out16, a16)
+    out._gd_bf16 = (out16, out._version)
+    if a16 is not None:
+        a._gd_bf16 = (a16, a._version)
+    return out
+
+
 def _scale_layout(x, s):
     """(s as fp32 [Bs, 1, Cs], batch stride, channel stride) when the HIP
     kernel (csrc/residual.hip) takes x [B, N, C] and this broadcast of s,

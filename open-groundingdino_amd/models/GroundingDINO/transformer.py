@@ -25,7 +25,7 @@ from torch import Tensor, nn
 from gdino_amd import kernels
 from gdino_amd.layernorm import add_norm, add_norm3
 from gdino_amd.mha import MultiheadAttention
-from gdino_amd.misc import box_refine, device_const, inverted, no_padding, padding_free, topk_indices
+from gdino_amd.misc import add_with_twins, box_refine, device_const, inverted, no_padding, padding_free, topk_indices
 
 from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
@@ -445,7 +445,9 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return add_norm(self.norm2, src if resid is None else resid, self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, key_padding_mask=None):
-        query = self.with_pos_embed(src, pos)
+        # src + pos with the bf16 twins of query and src (the projections'
+        # autocast inputs) in the same pass (gdino_amd.misc.add_with_twins)
+        query = src if pos is None else add_with_twins(src, pos)
         sa = self.self_attn
         if sa.identity_add and sa.batch_first and _inert(self.dropout1):
             # norm1(src + dropout1(dropout(msda(query)) + query)) with dropout1

@@ -1184,3 +1184,22 @@ def test_emulated_add_norm_two_handles(three):
                                                                                      norm.bias.grad.clone()]
     for a, b in zip(out[2], out[1]):
         assert E.rel_err(a.float(), b.float()) < (1e-2 if a.dtype == torch.bfloat16 else 1e-6)
+
+
+def test_emulated_add_with_twins():
+    """gd_add_twin_forward: query = src + pos in fp32 (exact) with the bf16
+    twins of query and src written in the same pass (bitwise the casts), the
+    twins attached where wgrad.TokenLinear reads them; gradients pass through."""
+    from emu_product import emulated_product
+    from gdino_amd.misc import add_with_twins
+    g = torch.Generator().manual_seed(4)
+    a = torch.randn(2, 37, 256, generator=g).requires_grad_()
+    b = torch.randn(2, 37, 256, generator=g).requires_grad_()
+    with emulated_product(), torch.autocast("cpu", dtype=torch.bfloat16):
+        q = add_with_twins(a, b)
+    assert torch.equal(q, a + b)
+    assert torch.equal(q._gd_bf16[0], (a + b).detach().to(torch.bfloat16)) and q._gd_bf16[1] == q._version
+    assert torch.equal(a._gd_bf16[0], a.detach().to(torch.bfloat16))
+    gq = torch.randn(2, 37, 256, generator=g)
+    q.backward(gq)
+    assert torch.equal(a.grad, gq) and torch.equal(b.grad, gq)
