@@ -537,16 +537,26 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
     // (n, m) slots of it fit (GD_MSDA_COUNT_PRIV=0: all global atomics, A/B)
     const int c23 = (pl.G.H[2] + 1) * (pl.G.W[2] + 1) + (pl.G.H[3] + 1) * (pl.G.W[3] + 1);
     const bool priv = Lq >= 64 && 2 * c23 <= kCountBins && env_int("GD_MSDA_COUNT_PRIV", 1) != 0;
-    if (priv)
-      hipLaunchKernelGGL(msda_bwd_count<true>, dim3((units + 63) / 64), dim3(256), 0, s, (const float*)loc, cnt, stat,
-                         pl.G, Lq, M, units);
+    // 4 rounds of 64 units per workgroup when a workgroup's 256 units still
+    // span at most two (n, m) (GD_MSDA_COUNT_R=1: one round, A/B)
+    const bool r4 = Lq >= 256 && env_int("GD_MSDA_COUNT_R", 4) == 4;
+    const int cu = r4 ? 256 : 64;
+    const dim3 cg((units + cu - 1) / cu);
+    if (priv && r4)
+      hipLaunchKernelGGL((msda_bwd_count<true, 4>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
+                         units);
+    else if (priv)
+      hipLaunchKernelGGL((msda_bwd_count<true, 1>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
+                         units);
+    else if (r4)
+      hipLaunchKernelGGL((msda_bwd_count<false, 4>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
+                         units);
     else
-      hipLaunchKernelGGL(msda_bwd_count<false>, dim3((units + 63) / 64), dim3(256), 0, s, (const float*)loc, cnt,
-                         stat, pl.G, Lq, M, units);
+      hipLaunchKernelGGL((msda_bwd_count<false, 1>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
+                         units);
     GD_LAUNCH_CHECK("msda_bwd_count");
   }
   hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);
-  hipLaunchKernelGGL(scan_bsums, dim3(1), dim3(256), 0, s, bsum, pl.nb);
   hipLaunchKernelGGL(scan_finish, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, (const int*)bsum, off,
                      cur);
   GD_LAUNCH_CHECK("msda_bwd scan");

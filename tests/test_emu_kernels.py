@@ -163,6 +163,18 @@ def test_emulated_sorted_backward_lds_histograms(priv, monkeypatch):
         _check_sorted(inputs, MEDIUM, 1e-5)
 
 
+@pytest.mark.parametrize("rounds", ["1", "4"])
+def test_emulated_sorted_backward_count_rounds(rounds, monkeypatch):
+    """The count pass with 4 rounds of 64 units per workgroup (the default
+    when Lq >= 256: MEDIUM's 380 queries, a ragged last workgroup, units of
+    two (n, m) in one histogram) and with one round (GD_MSDA_COUNT_R=1); the
+    7 216 cells of a batch of 2 span two scan blocks."""
+    monkeypatch.setenv("GD_MSDA_COUNT_R", rounds)
+    S = sum(h * w for h, w in MEDIUM)
+    inputs = _levels_inputs(MEDIUM, 2, S, seed=31, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
+    _check_sorted(inputs, MEDIUM, 1e-5)
+
+
 def test_emulated_sorted_backward_sweep_record_prefetch(monkeypatch):
     """GD_MSDA_SWEEP_PF=1: the sweep loads a row's first records during the
     previous row's exchange."""

@@ -223,6 +223,7 @@ BWD_VARIANTS = [
     ("sorted sweep-prefetch", {"GD_MSDA_BWD": "sorted", "GD_MSDA_SWEEP_PF": "1"}),
     ("sorted no-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "0"}),
     ("sorted forced-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "2"}),
+    ("sorted count-r1", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_R": "1"}),
     ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
     ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
     ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
@@ -253,7 +254,7 @@ def bwd_variants(iters, only_geom=None, only_variant=None):
                                                     "GD_MSDA_SORTED_K4", "GD_MSDA_SORTED_K1",
                                                     "GD_MSDA_SORTED_HP", "GD_MSDA_SWEEP_PF",
                                                     "GD_MSDA_COUNT_PRIV", "GD_MSDA_SORTED_LL",
-                                                    "GD_MSDA_SORTED_GS")}
+                                                    "GD_MSDA_SORTED_GS", "GD_MSDA_COUNT_R")}
             for k in saved:
                 os.environ.pop(k, None)
             os.environ.update(env)
