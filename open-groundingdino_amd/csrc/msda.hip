@@ -538,22 +538,24 @@ extern "C" gd_status gd_msda_backward_sorted(gd_dtype dt, const void* value, con
     const int c23 = (pl.G.H[2] + 1) * (pl.G.W[2] + 1) + (pl.G.H[3] + 1) * (pl.G.W[3] + 1);
     const bool priv = Lq >= 64 && 2 * c23 <= kCountBins && env_int("GD_MSDA_COUNT_PRIV", 1) != 0;
     // 4 rounds of 64 units per workgroup when a workgroup's 256 units still
-    // span at most two (n, m) (GD_MSDA_COUNT_R=1: one round, A/B)
-    const bool r4 = Lq >= 256 && env_int("GD_MSDA_COUNT_R", 4) == 4;
-    const int cu = r4 ? 256 : 64;
-    const dim3 cg((units + cu - 1) / cu);
-    if (priv && r4)
-      hipLaunchKernelGGL((msda_bwd_count<true, 4>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
-                         units);
-    else if (priv)
-      hipLaunchKernelGGL((msda_bwd_count<true, 1>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
-                         units);
-    else if (r4)
-      hipLaunchKernelGGL((msda_bwd_count<false, 4>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
-                         units);
-    else
-      hipLaunchKernelGGL((msda_bwd_count<false, 1>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M,
-                         units);
+    // span at most two (n, m) (GD_MSDA_COUNT_R=1: one round, =8: eight
+    // rounds when Lq >= 512 -- A/B)
+    const int renv = env_int("GD_MSDA_COUNT_R", 4);
+    const int rr = (renv == 8 && Lq >= 512) ? 8 : (renv >= 4 && Lq >= 256) ? 4 : 1;
+    const dim3 cg((units + 64 * rr - 1) / (64 * rr));
+#define GD_COUNT(PRIV, R)                                                                                      \
+  hipLaunchKernelGGL((msda_bwd_count<PRIV, R>), cg, dim3(256), 0, s, (const float*)loc, cnt, stat, pl.G, Lq, M, \
+                     units)
+    if (priv) {
+      if (rr == 8) GD_COUNT(true, 8);
+      else if (rr == 4) GD_COUNT(true, 4);
+      else GD_COUNT(true, 1);
+    } else {
+      if (rr == 8) GD_COUNT(false, 8);
+      else if (rr == 4) GD_COUNT(false, 4);
+      else GD_COUNT(false, 1);
+    }
+#undef GD_COUNT
     GD_LAUNCH_CHECK("msda_bwd_count");
   }
   hipLaunchKernelGGL(scan_block_sums, dim3(pl.nb), dim3(256), 0, s, (const int*)cnt, pl.ncells, bsum);

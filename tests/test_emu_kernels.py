@@ -163,16 +163,17 @@ def test_emulated_sorted_backward_lds_histograms(priv, monkeypatch):
         _check_sorted(inputs, MEDIUM, 1e-5)
 
 
-@pytest.mark.parametrize("rounds", ["1", "4"])
-def test_emulated_sorted_backward_count_rounds(rounds, monkeypatch):
+@pytest.mark.parametrize("rounds,levels", [("1", MEDIUM), ("4", MEDIUM), ("8", WIDE)])
+def test_emulated_sorted_backward_count_rounds(rounds, levels, monkeypatch):
     """The count pass with 4 rounds of 64 units per workgroup (the default
     when Lq >= 256: MEDIUM's 380 queries, a ragged last workgroup, units of
-    two (n, m) in one histogram) and with one round (GD_MSDA_COUNT_R=1); the
-    7 216 cells of a batch of 2 span two scan blocks."""
+    two (n, m) in one histogram), with one round (GD_MSDA_COUNT_R=1) and
+    with eight (=8, Lq >= 512: WIDE's 1 792 queries); the cells of a batch
+    of 2 span several scan blocks."""
     monkeypatch.setenv("GD_MSDA_COUNT_R", rounds)
-    S = sum(h * w for h, w in MEDIUM)
-    inputs = _levels_inputs(MEDIUM, 2, S, seed=31, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
-    _check_sorted(inputs, MEDIUM, 1e-5)
+    S = sum(h * w for h, w in levels)
+    inputs = _levels_inputs(levels, 2, S, seed=31, vdtype=torch.bfloat16, local=True, outlier_frac=0.05)
+    _check_sorted(inputs, levels, 1e-5)
 
 
 def test_emulated_sorted_backward_sweep_record_prefetch(monkeypatch):

@@ -224,6 +224,7 @@ BWD_VARIANTS = [
     ("sorted no-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "0"}),
     ("sorted forced-lds-histogram", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_PRIV": "2"}),
     ("sorted count-r1", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_R": "1"}),
+    ("sorted count-r8", {"GD_MSDA_BWD": "sorted", "GD_MSDA_COUNT_R": "8"}),
     ("sorted F1", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "1"}),
     ("sorted F4", {"GD_MSDA_BWD": "sorted-all", "GD_MSDA_SORTED_F": "4"}),
     ("sorted-all", {"GD_MSDA_BWD": "sorted-all"}),
