@@ -628,15 +628,20 @@ def _run(a, on_gpu, rank, world, local, ctrl):
             _progress("cpu baseline (host cores)")
             res["cpu_baseline"] = cpu_baseline(a.bs, recompute=a.checkpointing == "on")
         print(json.dumps(res), flush=True)
+    # free the step graph (and its shared memory pool) and drain the device
+    # while the HIP runtime and any profiler are still up, at every world
+    # size: left to interpreter teardown, a one-GPU graph was destroyed after
+    # the runtime began finalising (a SIGSEGV in a non-main thread under
+    # rocprofv3, profiles/r05p_pmc_write_segv.log).  Under DDP the captured
+    # step also holds RCCL collectives, and destroying a process group under
+    # a live graph that references it aborts.
+    if step_graph is not None:
+        step_graph.release()
+        step_graph = None
+    import gc
+    gc.collect()
+    _bounded_sync(on_gpu, a.timeout, "teardown")
     if world > 1:
-        # the captured step holds RCCL collectives: free it before the
-        # communicator goes (destroying a process group under a live graph
-        # that references it aborts)
-        if step_graph is not None:
-            step_graph.release()
-        import gc
-        gc.collect()
-        _bounded_sync(on_gpu, a.timeout, "teardown")
         _barrier(world, ctrl)
         dist.destroy_process_group()
     if not math.isfinite(loss_v):

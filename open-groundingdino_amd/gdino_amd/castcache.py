@@ -322,10 +322,17 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
 FUSED_RELU = os.environ.get("GDINO_FUSED_RELU", "1") != "0"
 
 
-def linear_relu(x: torch.Tensor, layer: nn.Linear) -> torch.Tensor:
+def linear_relu(x: torch.Tensor, layer: nn.Linear, fold_into_consumer: bool = False) -> torch.Tensor:
     """F.relu(layer(x)): on the token-linear route (GPU, bf16 autocast,
     trainable fp32 parameters) the ReLU runs in the GEMM's epilogue and its
-    backward masks by the saved output; elsewhere the plain composition."""
+    backward masks by the saved output; elsewhere the plain composition.
+
+    ``fold_into_consumer``: the CALLER guarantees that the result has exactly
+    one consumer, the next Linear (``ffn`` / utils.MLP own both layers);
+    that Linear may then fold this ReLU's backward into its dX kernel.
+    Without the promise the output is never offered for the fold, so a
+    second consumer always receives a correctly masked gradient (ADVICE
+    round 5)."""
     weight, bias = layer.weight, layer.bias
     dt = autocast_dtype(x) if ENABLED else None
     if FUSED_RELU and dt is not None and bias is not None and weight.is_floating_point():
@@ -334,8 +341,18 @@ def linear_relu(x: torch.Tensor, layer: nn.Linear) -> torch.Tensor:
         if route is not None:
             from . import wgrad
             return wgrad.token_linear(x, cached_cast(weight, dt), cached_cast(bias, dt), [weight], [bias],
-                                      route == "lib", relu=True)
+                                      route == "lib", relu=True, fold=fold_into_consumer)
     return F.relu(layer(x))
+
+
+def ffn(x: torch.Tensor, linear1: nn.Linear, linear2: nn.Module, dropout=None) -> torch.Tensor:
+    """linear2(dropout(relu(linear1(x)))) -- the FFN sublayer that owns both
+    Linears, so the ReLU output's only consumer is linear2 (through an
+    identity dropout) and its backward may be folded into linear2's dX."""
+    h = linear_relu(x, linear1, fold_into_consumer=True)
+    if dropout is not None:
+        h = dropout(h)
+    return linear2(h)
 
 
 class CachedCastLinear(nn.Linear):

@@ -21,6 +21,13 @@ What changes relative to the reference loop, and why:
     per-step ``.item()`` waits for the whole step and stalls the queue);
     a non-finite loss still stops training (at that check, as the
     reference's sys.exit(1));
+  * every read-back of the losses first waits for the device with a
+    deadline (``args.sync_timeout`` seconds, default 600): a replay stuck in
+    a collective or a hung kernel ends the run with a message and exit
+    status 3 instead of blocking forever (bench.py's ``_bounded_sync``);
+  * the weights at a non-finite-loss exit are NOT safe to save: up to
+    ``print_freq - 1`` replayed steps may already have applied the
+    non-finite update (the reference stops before its backward);
   * bf16 autocast (``args.amp``) needs no GradScaler;
   * the PAVE crop tiling of engine_multi.py:378-497 is product-specific and
     out of scope: batches are (samples, targets) or (samples, targets,
@@ -40,8 +47,9 @@ import sys
 import time
 
 import torch
+import torch.distributed as dist
 
-from .stepgraph import TrainStepGraph
+from .stepgraph import TrainStepGraph, make_control_group
 from .train import train_step
 
 
@@ -62,10 +70,40 @@ def _to_device(samples, targets, device):
     return samples, out
 
 
+class DeviceTimeout(RuntimeError):
+    """The device did not reach a read-back point within the deadline."""
+
+
+def bounded_wait(ready, timeout_s: float, what: str, poll_s: float = 2e-4):
+    """Poll ``ready()`` until it returns True, raising DeviceTimeout after
+    ``timeout_s`` seconds (the engine's analogue of bench._bounded_sync)."""
+    deadline = time.monotonic() + timeout_s
+    while not ready():
+        if time.monotonic() > deadline:
+            raise DeviceTimeout(f"device did not finish within {timeout_s:.0f} s: {what}")
+        time.sleep(poll_s)
+
+
+def _device_ready_fn(device):
+    """A readiness probe for the work queued so far on ``device``'s current
+    stream (always ready for host tensors)."""
+    if not (torch.cuda.is_available() and torch.device(device).type == "cuda"):
+        return lambda: True
+    ev = torch.cuda.Event()
+    ev.record()
+    return ev.query
+
+
 def step_graph_for(model, criterion, optimizer, max_norm, args=None, grad_sync=None, control_group=None):
-    """The TrainStepGraph cached on the model for this optimizer."""
+    """The TrainStepGraph cached on the model for this optimizer.  With N > 1
+    ranks and no ``control_group``, a gloo group is made here for the step
+    graph's host agreements (every rank reaches this call): on the default
+    NCCL group each agreement would be an eager collective plus a
+    device-wide wait per step."""
     g = getattr(model, "_gd_step_graph", None)
     if g is None or g.optimizer is not optimizer or g.criterion is not criterion:
+        if control_group is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            control_group = make_control_group()
         amp = torch.bfloat16 if getattr(args, "amp", True) else None
         g = TrainStepGraph(model, criterion, optimizer, clip_max_norm=max_norm, amp_dtype=amp,
                            grad_sync=grad_sync, control_group=control_group,
@@ -89,8 +127,15 @@ def train_one_epoch(model: torch.nn.Module, criterion: torch.nn.Module, data_loa
     header = f"Epoch: [{epoch}]"
     out = sys.stdout if logger is None else None
 
+    timeout_s = float(getattr(args, "sync_timeout", 600.0))
+
     def flush(i):
         nonlocal pending
+        try:
+            bounded_wait(_device_ready_fn(device), timeout_s, f"{header} loss read-back at step {i}")
+        except DeviceTimeout as e:
+            print(f"{e}; stopping training", file=sys.stderr, flush=True)
+            sys.exit(3)
         for loss, terms in pending:
             v = float(loss)
             if not math.isfinite(v):

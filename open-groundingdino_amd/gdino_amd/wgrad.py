@@ -237,7 +237,7 @@ class TokenLinear(torch.autograd.Function):
     matching bias blocks); gradients go to ``params`` in fp32."""
 
     @staticmethod
-    def forward(ctx, x, wc, bc, nw, lib_wgrad, relu, *params):
+    def forward(ctx, x, wc, bc, nw, lib_wgrad, relu, fold, *params):
         # the bf16 copy a producer wrote beside x (layernorm: ``_gd_bf16``)
         # instead of a cast kernel
         tw = getattr(x, "_gd_bf16", None)
@@ -259,7 +259,8 @@ class TokenLinear(torch.autograd.Function):
             # set by the consumer Linear when it folds this ReLU's backward
             # into its own dX (masked_dx): the gradient arrives masked
             ctx.relu_box = [False]
-            y._gd_relu_box = ctx.relu_box
+            if fold:  # the caller owns y's only consumer (castcache.ffn / MLP)
+                y._gd_relu_box = ctx.relu_box
             # x2: the rows the weight gradient reads (already copied once
             # when xc could not be viewed 2-D -- not again in the backward)
             ctx.save_for_backward(x2, wc, y)
@@ -277,6 +278,7 @@ class TokenLinear(torch.autograd.Function):
             ctx.mask_dx = xc is x and masked_dx_ok(x, wc)
             if ctx.mask_dx:
                 x._gd_relu_box[0] = True
+                del x._gd_relu_box  # claimed: no second consumer may fold it
         ctx.relu = relu
         ctx.lib_wgrad = lib_wgrad
         ctx.x_dtype = x.dtype
@@ -307,14 +309,17 @@ class TokenLinear(torch.autograd.Function):
         grads = list(dw.split(ctx.rows, 0))
         if ctx.has_bias:
             grads += list(db.split(ctx.rows, 0))
-        return (dx, None, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, None, *grads)
 
 
-def token_linear(x, wc, bc, weights, biases, lib_wgrad=False, relu=False):
+def token_linear(x, wc, bc, weights, biases, lib_wgrad=False, relu=False, fold=False):
     """F.linear(x, wc, bc) whose weight / bias gradients reach the fp32
     ``weights`` / ``biases`` (row blocks of wc / bc) through the split-K
     kernel (or, lib_wgrad, the library GEMM with fp32 output); ``relu``:
-    relu(F.linear(...)) with the activation in the GEMM epilogue."""
+    relu(F.linear(...)) with the activation in the GEMM epilogue; ``fold``
+    (relu only): the caller guarantees the output's only consumer is the next
+    Linear, which may then fold the ReLU backward into its dX kernel."""
     params = list(weights) + (list(biases) if bc is not None else [])
+    relu = bool(relu and bc is not None)
     return TokenLinear.apply(x, wc.detach(), None if bc is None else bc.detach(), len(weights), bool(lib_wgrad),
-                             bool(relu and bc is not None), *params)
+                             relu, bool(fold and relu), *params)

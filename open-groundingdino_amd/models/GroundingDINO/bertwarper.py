@@ -85,7 +85,8 @@ class BertModelWarper(nn.Module):
 
     def _fast_ok(self, hidden, head_mask) -> bool:
         """The frozen-encoder path: every encoder parameter frozen (cfg
-        freeze_keywords ['bert'], train.apply_freeze) or no autograd, bf16
+        freeze_keywords ['bert'], train.apply_freeze) and nothing upstream
+        needing a gradient, or no autograd; bf16
         autocast on the HIP device, the stock post-norm GELU BERT layout."""
         import os
         from gdino_amd import _lib, castcache
@@ -96,7 +97,10 @@ class BertModelWarper(nn.Module):
                 and cfg.hidden_act == "gelu" and not getattr(cfg, "is_decoder", False)
                 and cfg.hidden_size in WIDTHS and cfg.hidden_size % cfg.num_attention_heads == 0
                 and (cfg.hidden_size // cfg.num_attention_heads) in (32, 64)
-                and (not torch.is_grad_enabled() or not any(p.requires_grad for p in self.encoder.parameters())))
+                and (not torch.is_grad_enabled() or not any(p.requires_grad for p in self.encoder.parameters()))
+                # trainable embeddings (a partial freeze) need the module
+                # stack: the frozen path runs under no_grad
+                and not (torch.is_grad_enabled() and hidden.requires_grad))
 
     def _encode_frozen(self, hidden, keep):
         """The 12 BertLayers (transformers modeling_bert BertLayer: self

@@ -31,7 +31,7 @@ from .fuse_modules import BiAttentionBlock
 from .ms_deform_attn import MultiScaleDeformableAttention as MSDeformAttn
 from .ms_deform_attn import msda_attend
 from .transformer_vanilla import TransformerEncoderLayer
-from .utils import (MLP, _get_activation_fn, _get_clones, ffn_act, gen_encoder_output_proposals,
+from .utils import (MLP, _get_activation_fn, _get_clones, ffn, gen_encoder_output_proposals,
                     get_sine_pos_embed, query_anchors)
 
 _DEBUG_NAN = os.environ.get("GDINO_DEBUG_NAN", "0") == "1"
@@ -441,7 +441,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src, resid=None):
         """resid: a second handle on src (add_norm taps) for the residual"""
-        src2 = self.linear2(self.dropout2(ffn_act(self.linear1, self.activation, src)))
+        src2 = ffn(self.linear1, self.activation, self.dropout2, self.linear2, src)
         return add_norm(self.norm2, src if resid is None else resid, self.dropout3(src2))
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, key_padding_mask=None):
@@ -506,7 +506,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         # the reference runs the decoder FFN outside autocast (fp32, :870-875)
         with torch.autocast(device_type=tgt.device.type, enabled=False):
             t = tgt.float() if tgt.dtype in (torch.float16, torch.bfloat16) else tgt
-            tgt2 = self.linear2(self.dropout3(ffn_act(self.linear1, self.activation, t)))
+            tgt2 = ffn(self.linear1, self.activation, self.dropout3, self.linear2, t)
         return add_norm(self.norm3, tgt if resid is None else resid, self.dropout4(tgt2))
 
     def forward(self, tgt, tgt_query_pos=None, tgt_query_sine_embed=None, tgt_key_padding_mask=None,

@@ -9,7 +9,7 @@ from torch import Tensor, nn
 from gdino_amd.layernorm import add_norm
 from gdino_amd.mha import MultiheadAttention
 
-from .utils import _get_activation_fn, _get_clones, ffn_act
+from .utils import _get_activation_fn, _get_clones, ffn
 
 
 class TransformerEncoderLayer(nn.Module):
@@ -41,7 +41,7 @@ class TransformerEncoderLayer(nn.Module):
         qk = src if pos is None else src + pos
         attn = self.self_attn(qk, qk, value=src, attn_mask=src_mask)[0]
         src = add_norm(self.norm1, src, self.dropout1(attn))
-        ffn = self.linear2(self.dropout(ffn_act(self.linear1, self.activation, src)))
+        ffn = ffn(self.linear1, self.activation, self.dropout, self.linear2, src)
         return add_norm(self.norm2, src, self.dropout2(ffn))
 
 

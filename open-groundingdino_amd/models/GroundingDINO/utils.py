@@ -145,7 +145,8 @@ class MLP(nn.Module):
         # route (castcache.linear_relu; elsewhere the plain composition)
         last = self.num_layers - 1
         for i, layer in enumerate(self.layers):
-            x = castcache.linear_relu(x, layer) if i < last else layer(x)
+            # (the MLP owns both layers: layer i's output feeds only layer i+1)
+            x = castcache.linear_relu(x, layer, fold_into_consumer=True) if i < last else layer(x)
         return x
 
 
@@ -161,11 +162,23 @@ def _get_activation_fn(activation, d_model=256, batch_dim=0):
 def ffn_act(linear1, activation, x):
     """activation(linear1(x)) of the FFN sublayers (reference transformer.py
     forward_ffn, transformer_vanilla.py:83).  With ReLU on the GPU training
-    path the activation runs in the GEMM epilogue (castcache.linear_relu)."""
+    path the activation runs in the GEMM epilogue (castcache.linear_relu);
+    the output is not offered to a consumer's dX fold (use ``ffn``)."""
     if activation is F.relu:
         from gdino_amd.castcache import linear_relu
         return linear_relu(x, linear1)
     return activation(linear1(x))
+
+
+def ffn(linear1, activation, dropout, linear2, x):
+    """linear2(dropout(activation(linear1(x)))), the FFN sublayer (reference
+    transformer.py:803-806,931-934, transformer_vanilla.py:83).  With ReLU the
+    sublayer owns both Linears, so linear2's dX kernel may apply the ReLU's
+    backward mask (castcache.ffn)."""
+    if activation is F.relu:
+        from gdino_amd.castcache import ffn as _ffn
+        return _ffn(x, linear1, linear2, dropout)
+    return linear2(dropout(activation(linear1(x))))
 
 
 class ContrastiveEmbed(nn.Module):

@@ -1155,15 +1155,88 @@ def test_emulated_relu_linear_pair_folds_the_threshold(monkeypatch):
         ps = [t.clone().requires_grad_() for t in (w1, b1, w2, b2)]
         with emulated_product():
             h = wgrad.token_linear(x, ps[0].to(torch.bfloat16), ps[1].to(torch.bfloat16), [ps[0]], [ps[1]],
-                                   relu=True)
+                                   relu=True, fold=True)
+            box = h._gd_relu_box
             y = wgrad.token_linear(h, ps[2].to(torch.bfloat16), ps[3].to(torch.bfloat16), [ps[2]], [ps[3]])
             (y.float() * gy).sum().backward()
-        return h._gd_relu_box[0], [x.grad] + [p.grad for p in ps]
+        return box[0], [x.grad] + [p.grad for p in ps]
 
     (folded, got), (unfolded, ref) = run(True), run(False)
     assert folded and not unfolded
     for a, b in zip(got, ref):
         assert float((a.float() - b.float()).abs().max()) <= 2e-2 * float(b.float().abs().max())
+
+
+@pytest.mark.parametrize("second", ["elementwise", "linear"])
+def test_emulated_relu_output_with_a_second_consumer(monkeypatch, second):
+    """a relu TokenLinear whose output has a second consumer
+    besides the next Linear.  Without the caller's single-consumer promise
+    (fold=False, the default of castcache.linear_relu) the output is never
+    offered for the dX fold, so both consumers' gradients pass the ReLU mask:
+    every gradient matches the plain fp32 composition.  A claimed tag is
+    removed, so a second Linear consumer can never fold the same ReLU."""
+    from emu_product import emulated_product
+    from gdino_amd import wgrad
+    monkeypatch.setattr(wgrad, "TLIN_MASKED_MIN_TOKENS", 64)
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.randn(2, 96, 64, generator=g)
+    w1, b1 = torch.randn(128, 64, generator=g) * 0.125, torch.randn(128, generator=g) * 0.1
+    w2, b2 = torch.randn(64, 128, generator=g) * 0.09, torch.randn(64, generator=g) * 0.1
+    w3 = torch.randn(32, 128, generator=g) * 0.09
+    gy, gz = torch.randn(2, 96, 64, generator=g), torch.randn(2, 96, 128 if second == "elementwise" else 32,
+                                                             generator=g)
+
+    def consumers(h, ps, lin):
+        y = lin(h, ps[2], ps[3])
+        z = h.float() * 3.0 if second == "elementwise" else lin(h, ps[4], None)
+        return (y.float() * gy).sum() + (z.float() * gz).sum()
+
+    def run(masked):
+        monkeypatch.setattr(wgrad, "TLIN_MASKED", masked)
+        x = x0.to(torch.bfloat16).requires_grad_()
+        ps = [t.clone().requires_grad_() for t in (w1, b1, w2, b2, w3)]
+        with emulated_product():
+            h = wgrad.token_linear(x, ps[0].to(torch.bfloat16), ps[1].to(torch.bfloat16), [ps[0]], [ps[1]],
+                                   relu=True)
+            assert getattr(h, "_gd_relu_box", None) is None  # not offered without the promise
+
+            def lin(t, w, b):
+                return wgrad.token_linear(t, w.to(torch.bfloat16), None if b is None else b.to(torch.bfloat16),
+                                          [w], [] if b is None else [b])
+            consumers(h, ps, lin).backward()
+        return x, ps, [x.grad] + [p.grad for p in ps]
+
+    # the fold enabled (what the second consumer would have broken) vs the
+    # unfused threshold path: the same gradients
+    x, ps, got = run(True)
+    _, _, ref = run(False)
+    for a, b in zip(got, ref):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert float((a.float() - b.float()).abs().max()) <= 1e-6 * float(b.float().abs().max())
+    # and both follow the fp64 composition (the ReLU mask taken from the
+    # product's bf16 pre-activation, so boundary elements agree)
+    xr = x0.to(torch.bfloat16).double().requires_grad_()
+    pr = [t.double().requires_grad_() for t in (w1, b1, w2, b2, w3)]
+    pre = torch.nn.functional.linear(xr, pr[0], pr[1])
+    with torch.no_grad(), emulated_product():
+        hp = wgrad.token_linear(x.detach(), ps[0].detach().to(torch.bfloat16), ps[1].detach().to(torch.bfloat16),
+                                [ps[0]], [ps[1]], relu=True)
+    hr = pre * (hp > 0)
+    consumers(hr, pr, lambda t, w, b: torch.nn.functional.linear(t, w, b)).backward()
+    for a, b in zip(got, [xr.grad] + [p.grad for p in pr]):
+        if a is not None:
+            assert float((a.double() - b).abs().max()) <= 3e-2 * float(b.abs().max())
+
+    # a claimed tag is gone: the second Linear consumer cannot fold again
+    monkeypatch.setattr(wgrad, "TLIN_MASKED", True)
+    with emulated_product():
+        h = wgrad.token_linear(x.detach(), ps[0].detach().to(torch.bfloat16), ps[1].detach().to(torch.bfloat16),
+                               [ps[0]], [ps[1]], relu=True, fold=True)
+        box = h._gd_relu_box
+        wgrad.token_linear(h, ps[2].detach().to(torch.bfloat16), ps[3].detach().to(torch.bfloat16), [ps[2]],
+                           [ps[3]])
+        assert box[0] and getattr(h, "_gd_relu_box", None) is None
 
 
 @pytest.mark.parametrize("three", [False, True])

@@ -254,3 +254,42 @@ def test_frozen_bert_fast_encoder_matches_the_layer_stack():
         assert fast.grad_fn is None and fast.dtype == ref.dtype == torch.float32
         rel = float((fast - ref).norm() / ref.norm())
         assert rel < tol, (n, rel)
+
+
+def test_frozen_bert_fast_path_keeps_trainable_embedding_gradients():
+    """with the encoder frozen but the embeddings trainable
+    (a partial freeze), the fast path (which runs under no_grad) is refused,
+    so the output keeps its autograd graph back to the embeddings; with
+    nothing upstream needing a gradient it is taken."""
+    from gdino_amd.config import make_args
+    from gdino_amd.train import build_training
+    torch.manual_seed(0)
+    model, _, _, _ = build_training(make_args(device="cpu", enc_layers=1, dec_layers=1, num_queries=100),
+                                    torch.device("cpu"))
+    bert = model.bert
+    bert.train()
+    for m in bert.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    assert not any(p.requires_grad for p in bert.encoder.parameters())
+    bert.encoder.layer = bert.encoder.layer[:2]
+    ids = torch.randint(1000, 2000, (2, 24))
+    kw = dict(input_ids=ids, attention_mask=torch.ones(2, 24, 24, dtype=torch.bool),
+              token_type_ids=torch.zeros_like(ids), position_ids=torch.arange(24)[None].repeat(2, 1))
+    taken = []
+    orig = type(bert)._fast_ok
+
+    def spy(self, hidden, head_mask):
+        r = orig(self, hidden, head_mask)
+        taken.append(r)
+        return r
+    type(bert)._fast_ok = spy
+    try:
+        for trainable in (False, True):
+            bert.embeddings.word_embeddings.weight.requires_grad_(trainable)
+            with emu_product.emulated_product(), torch.autocast("cpu", dtype=torch.bfloat16):
+                out = bert(**kw)["last_hidden_state"]
+            assert (out.grad_fn is not None) == trainable
+    finally:
+        type(bert)._fast_ok = orig
+    assert taken == [True, False]
