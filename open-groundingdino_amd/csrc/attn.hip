@@ -15,6 +15,7 @@
 namespace gd {
 namespace {
 #include "attn_kernels.inc"
+#include "attn_ks.inc"
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
@@ -85,6 +86,16 @@ int key_tiles(int Lk, int bh) {
   return int64_t((Lk + 31) / 32) * bh >= 1024 ? 2 : 1;
 }
 
+// The split kernels (attn_ks.inc: a workgroup per 16-query / 16-key tile,
+// its waves splitting the other dimension) where the one-walk kernels would
+// run 16-token waves -- the small (b, h) x L problems of the train step:
+// decoder self / text cross-attention, BERT, text enhancer.  GD_ATTN_SPLIT=0
+// keeps the round-5 kernels (A/B).
+bool use_split(int L, int bh) {
+  if (env_int("GD_ATTN_SPLIT", 1) == 0) return false;
+  return int64_t((L + 63) / 64) * bh < 1024;
+}
+
 }  // namespace
 }  // namespace gd
 
@@ -112,6 +123,24 @@ extern "C" gd_status gd_attn_forward_dev(gd_dtype dt, int B, int H, int Lq, int 
   a.o = out;
   a.lse = lse;
   hipStream_t s = as_hip(stream);
+  if (use_split(Lq, B * H)) {
+    const dim3 g16(unsigned((Lq + 15) / 16), unsigned(B * H));
+#define GD_AS1(T, HD, KS)                                                                       \
+  do {                                                                                          \
+    if (a.dropout)                                                                              \
+      hipLaunchKernelGGL((attn_fwd_ks_kernel<T, HD, true, KS>), g16, dim3(64 * KS), 0, s, a);   \
+    else                                                                                        \
+      hipLaunchKernelGGL((attn_fwd_ks_kernel<T, HD, false, KS>), g16, dim3(64 * KS), 0, s, a);  \
+  } while (0)
+    if (dt == GD_BF16) {
+      if (head_dim == 32) GD_AS1(uint16_t, 32, 4); else GD_AS1(uint16_t, 64, 4);
+    } else {
+      if (head_dim == 32) GD_AS1(float, 32, 2); else GD_AS1(float, 64, 2);
+    }
+#undef GD_AS1
+    GD_LAUNCH_CHECK("attn_fwd_ks");
+    return GD_OK;
+  }
   const int qt = query_tiles(Lq, B * H);
   const dim3 grid(unsigned((Lq + 64 * qt - 1) / (64 * qt)), unsigned(B * H));
 #define GD_AF1(T, HD, QT)                                                                    \
@@ -176,6 +205,30 @@ extern "C" gd_status gd_attn_backward_dev(gd_dtype dt, int B, int H, int Lq, int
   a.lse = const_cast<float*>(lse);
   a.dsum = dsum;
   hipStream_t s = as_hip(stream);
+  const bool split_q = use_split(Lq, B * H), split_k = use_split(Lk, B * H);
+  if (split_q && split_k) {
+    const dim3 gq16(unsigned((Lq + 15) / 16), unsigned(B * H)), gk16(unsigned((Lk + 15) / 16), unsigned(B * H));
+#define GD_BS1(T, HD, DR, KS)                                                                              \
+  do {                                                                                                     \
+    hipLaunchKernelGGL((attn_bwd_dq_ks_kernel<T, HD, DR, KS>), gq16, dim3(64 * KS), 0, s, a);              \
+    GD_LAUNCH_CHECK("attn_bwd_dq_ks");                                                                     \
+    hipLaunchKernelGGL((attn_bwd_dkv_qs_kernel<T, HD, DR, KS>), gk16, dim3(64 * KS), 0, s, a);             \
+    GD_LAUNCH_CHECK("attn_bwd_dkv_qs");                                                                    \
+  } while (0)
+#define GD_BS(T, HD, KS)                     \
+  do {                                       \
+    if (a.dropout) GD_BS1(T, HD, true, KS);  \
+    else GD_BS1(T, HD, false, KS);           \
+  } while (0)
+    if (dt == GD_BF16) {
+      if (head_dim == 32) GD_BS(uint16_t, 32, 4); else GD_BS(uint16_t, 64, 4);
+    } else {
+      if (head_dim == 32) GD_BS(float, 32, 2); else GD_BS(float, 64, 2);
+    }
+#undef GD_BS1
+#undef GD_BS
+    return GD_OK;
+  }
   const int qt = query_tiles(Lq, B * H), kt = key_tiles(Lk, B * H);
   const dim3 gq(unsigned((Lq + 64 * qt - 1) / (64 * qt)), unsigned(B * H));
   const dim3 gk(unsigned((Lk + 64 * kt - 1) / (64 * kt)), unsigned(B * H));

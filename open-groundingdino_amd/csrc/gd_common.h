@@ -151,6 +151,20 @@ __device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
     __builtin_amdgcn_s_barrier();             \
     __asm__ __volatile__("" ::: "memory");    \
   } while (0)
+// Wave-level ordering point for wave-private LDS: the wave runs in lock step
+// and a wave's LDS instructions execute in order, so a ds_write by one lane
+// is visible to a later ds_read by another lane of the same wave; this only
+// keeps the compiler from moving LDS accesses across the point (no
+// s_barrier, no wait).  tests/emu's header defines it as a wave-wide
+// rendezvous of its lane fibers.
+#ifndef gd_wave_sync
+#define gd_wave_sync()                        \
+  do {                                        \
+    __asm__ __volatile__("" ::: "memory");    \
+    __builtin_amdgcn_wave_barrier();          \
+    __asm__ __volatile__("" ::: "memory");    \
+  } while (0)
+#endif
 }  // namespace gd
 
 // integer tuning / A-B switch from the environment (host side)

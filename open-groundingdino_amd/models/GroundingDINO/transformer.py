@@ -304,6 +304,14 @@ class TransformerEncoder(nn.Module):
 DEFER_BOX_REFINE = os.environ.get("GDINO_DEFER_BOX_REFINE", "1") != "0"
 
 
+def _uncached_autocast(dev: str):
+    """The current autocast state with its cast cache disabled (a no-op
+    context when autocast is off)."""
+    if dev not in ("cuda", "cpu") or not torch.is_autocast_enabled(dev):
+        return contextlib.nullcontext()
+    return torch.autocast(device_type=dev, dtype=torch.get_autocast_dtype(dev), cache_enabled=False)
+
+
 class _BatchedBoxRefine(torch.autograd.Function):
     """The decoder's refined anchors new_ref[l] = box_refine(bbox_embed(
     out[l]), ref[l]) of every layer (reference transformer.py
@@ -397,7 +405,11 @@ class TransformerDecoder(nn.Module):
                 if deferred is not None:
                     # the anchor update without autograd; its gradient path
                     # is rebuilt for all layers at once below
-                    with torch.no_grad():
+                    # (autocast's weight-cast cache off: a cast made here,
+                    # without autograd, would be reused by the model's box
+                    # heads in the same autocast region and cut their
+                    # gradient to bbox_embed's weights)
+                    with torch.no_grad(), _uncached_autocast(output.device.type):
                         new_ref = box_refine(self.bbox_embed[layer_id](output), reference_points)
                     deferred.append((output, reference_points, new_ref))
                 else:

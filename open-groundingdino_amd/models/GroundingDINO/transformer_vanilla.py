@@ -41,8 +41,8 @@ class TransformerEncoderLayer(nn.Module):
         qk = src if pos is None else src + pos
         attn = self.self_attn(qk, qk, value=src, attn_mask=src_mask)[0]
         src = add_norm(self.norm1, src, self.dropout1(attn))
-        ffn = ffn(self.linear1, self.activation, self.dropout, self.linear2, src)
-        return add_norm(self.norm2, src, self.dropout2(ffn))
+        y = ffn(self.linear1, self.activation, self.dropout, self.linear2, src)
+        return add_norm(self.norm2, src, self.dropout2(y))
 
 
 class TextTransformer(nn.Module):

@@ -279,6 +279,16 @@ inline void wave_gather(const void* mine, size_t nbytes, void* all) {
   }
 }
 
+// __builtin_amdgcn_wave_barrier (gd_common.h gd_wave_sync): no lane of the
+// wave continues before every lane has arrived (an exchange of nothing), so
+// wave-private LDS written by one lane and read by another is ordered as the
+// lock-stepped wave orders it on the GPU
+inline void wave_sync() {
+  const uint8_t z = 0;
+  uint8_t all[64];
+  wave_gather(&z, 1, all);
+}
+
 // __ballot: bit i = predicate of lane i (all 64 lanes of the wave take part)
 inline unsigned long long ballot(int pred) {
   const uint8_t mine = pred ? 1 : 0;
@@ -398,6 +408,7 @@ inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 #define __shfl(v, src, width) ::gd_emu::shfl((v), (src), (width))
 #define __builtin_amdgcn_readlane(v, src) ::gd_emu::readlane((v), (src))
 #define __builtin_amdgcn_s_barrier() ::gd_emu::syncthreads()
+#define gd_wave_sync() ::gd_emu::wave_sync()
 #define __builtin_amdgcn_s_waitcnt(imm) ((void)(imm))  // memory is synchronous here
 #define GD_LDS_DMA16(src, dst) ::gd_emu::lds_dma16((const void*)(src), (void*)(dst))
 // compiler scheduling hints: no semantics to emulate

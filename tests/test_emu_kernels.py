@@ -677,15 +677,18 @@ def test_emulated_attention(B, H, Lq, Lk, hd, mask_kind, dtype, tol, layout):
         assert E.rel_err(mine.double(), r) < tol * 2, name
 
 
-@pytest.mark.parametrize("qt,kt", [("4", "2"), ("1", "1"), ("4", "1"), ("1", "2")])
-def test_emulated_attention_wave_tilings(qt, kt, monkeypatch):
-    """Both query-tile widths of the forward / dQ kernels (64 or 16 queries
-    per wave) and both key-tile widths of the dK / dV kernel (32 or 16 keys
-    per wave), forced with GD_ATTN_QT / GD_ATTN_KT: identical math, ragged
-    lengths on both sides."""
+@pytest.mark.parametrize("qt,kt,split", [("4", "2", "0"), ("1", "1", "0"), ("4", "1", "0"), ("1", "2", "0"),
+                                          ("0", "0", "1")])
+def test_emulated_attention_wave_tilings(qt, kt, split, monkeypatch):
+    """Both query-tile widths of the one-walk forward / dQ kernels (64 or 16
+    queries per wave) and both key-tile widths of their dK / dV kernel (32 or
+    16 keys per wave), forced with GD_ATTN_QT / GD_ATTN_KT under
+    GD_ATTN_SPLIT=0, and the split kernels (attn_ks.inc, the default at
+    these sizes): identical math, ragged lengths on both sides."""
     from oracle.blocks import attention_ref
     monkeypatch.setenv("GD_ATTN_QT", qt)
     monkeypatch.setenv("GD_ATTN_KT", kt)
+    monkeypatch.setenv("GD_ATTN_SPLIT", split)
     q, k, v, mask, scale, grad = _attn_case(2, 2, 150, 90, 32, "bool", torch.float32, seed=11, layout="blh")
     out, lse = E.attn_forward(q, k, v, mask, scale)
     qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))

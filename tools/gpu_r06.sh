@@ -1,0 +1,59 @@
+# round 6 GPU sessions: gpurun --timeout 1200 -- bash tools/gpu_r06.sh <mode>
+# every GPU step under its own time limit, chained with && (the first
+# failure ends the call; no retries)
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T() { timeout -k 10 "$@"; }
+step() { echo "[$(date +%T)] $*"; }
+PROF=/tmp/gd_prof
+MODE="${1:-a}"
+PMC_A="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
+PMC_B="SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"
+
+mfma_pmc() {  # tag, microbench args...
+  local tag=$1; shift
+  step "attn microbench ($tag)" &&
+  T 300 python3 tools/attn_microbench.py "$@" > gpurun_out/${tag}_mb.jsonl 2>&1 &&
+  step "pmc A ($tag)" &&
+  T 240 rocprofv3 --pmc $PMC_A --kernel-trace --output-format csv -d "$PROF/${tag}_a" -o run -- \
+      python3 tools/attn_microbench.py --iters 3 --warmup 1 "$@" > gpurun_out/${tag}_pmc_a.log 2>&1 &&
+  step "pmc B ($tag)" &&
+  T 240 rocprofv3 --pmc $PMC_B --kernel-trace --output-format csv -d "$PROF/${tag}_b" -o run -- \
+      python3 tools/attn_microbench.py --iters 3 --warmup 1 "$@" > gpurun_out/${tag}_pmc_b.log 2>&1 &&
+  python3 tools/mfma_counters.py --pass "$PROF/${tag}_a" --pass "$PROF/${tag}_b" --bench gpurun_out/${tag}_mb.jsonl \
+      --note "$tag" --out gpurun_out/${tag}_mfma_counters.json > gpurun_out/${tag}_mfma_counters.txt 2>&1
+}
+
+case "$MODE" in
+a)
+  # baseline of the round: GPU suite, smoke, driver bench, MFMA counters
+  step "pytest -m gpu" &&
+  T 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/a_gpu_tests.log 2>&1 &&
+  step "smoke" &&
+  T 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/a_smoke.log 2>&1 &&
+  step "bench (driver command)" &&
+  T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/a_bench.log 2>&1 &&
+  mfma_pmc a
+  ;;
+mb)
+  mfma_pmc mb "${@:2}"
+  ;;
+attn)
+  # attention-family parity on the GPU, then the microbench + counters
+  step "pytest attention" &&
+  T 600 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py -m gpu -x -q --timeout 120 \
+      --timeout-method thread -k "attention or block" > gpurun_out/attn_tests.log 2>&1 &&
+  mfma_pmc attn --cases attn
+  ;;
+bench)
+  step "bench (driver command)" &&
+  T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1
+  ;;
+*)
+  echo "usage: $0 a|mb|bench" >&2; exit 2 ;;
+esac
+rc=$?
+step "done rc=$rc"
+exit $rc
