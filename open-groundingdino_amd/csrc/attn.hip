@@ -46,6 +46,11 @@ gd_status fill(AttnArgs& a, gd_dtype dt, int B, int H, int Lq, int Lk, int hd, c
     a.vs[i] = vs[i];
   }
   for (int i = 0; i < 3; ++i) a.ms[i] = mask_kind ? ms[i] : 0;
+  {
+    const uintptr_t mal = mask_kind == 2 ? 15 : 3;
+    a.mvec = mask_kind != 0 && (reinterpret_cast<uintptr_t>(mask) & mal) == 0 && a.ms[0] % 4 == 0 &&
+             a.ms[1] % 4 == 0 && a.ms[2] % 4 == 0;
+  }
   a.B = B;
   a.H = H;
   a.Lq = Lq;
@@ -125,12 +130,18 @@ extern "C" gd_status gd_attn_forward_dev(gd_dtype dt, int B, int H, int Lq, int 
   hipStream_t s = as_hip(stream);
   if (use_split(Lq, B * H)) {
     const dim3 g16(unsigned((Lq + 15) / 16), unsigned(B * H));
-#define GD_AS1(T, HD, KS)                                                                       \
-  do {                                                                                          \
-    if (a.dropout)                                                                              \
-      hipLaunchKernelGGL((attn_fwd_ks_kernel<T, HD, true, KS>), g16, dim3(64 * KS), 0, s, a);   \
-    else                                                                                        \
-      hipLaunchKernelGGL((attn_fwd_ks_kernel<T, HD, false, KS>), g16, dim3(64 * KS), 0, s, a);  \
+#define GD_AS2(T, HD, KS, MK)                                                                     \
+  do {                                                                                            \
+    if (a.dropout)                                                                                \
+      hipLaunchKernelGGL((attn_fwd_ks_kernel<T, HD, true, KS, MK>), g16, dim3(64 * KS), 0, s, a);  \
+    else                                                                                          \
+      hipLaunchKernelGGL((attn_fwd_ks_kernel<T, HD, false, KS, MK>), g16, dim3(64 * KS), 0, s, a); \
+  } while (0)
+#define GD_AS1(T, HD, KS)                                  \
+  do {                                                     \
+    if (a.mask_kind == 1) GD_AS2(T, HD, KS, 1);            \
+    else if (a.mask_kind == 2) GD_AS2(T, HD, KS, 2);       \
+    else GD_AS2(T, HD, KS, 0);                             \
   } while (0)
     if (dt == GD_BF16) {
       if (head_dim == 32) GD_AS1(uint16_t, 32, 4); else GD_AS1(uint16_t, 64, 4);
@@ -138,6 +149,7 @@ extern "C" gd_status gd_attn_forward_dev(gd_dtype dt, int B, int H, int Lq, int 
       if (head_dim == 32) GD_AS1(float, 32, 2); else GD_AS1(float, 64, 2);
     }
 #undef GD_AS1
+#undef GD_AS2
     GD_LAUNCH_CHECK("attn_fwd_ks");
     return GD_OK;
   }
@@ -204,16 +216,23 @@ extern "C" gd_status gd_attn_backward_dev(gd_dtype dt, int B, int H, int Lq, int
   a.dv = grad_v;
   a.lse = const_cast<float*>(lse);
   a.dsum = dsum;
+  a.lvec = Lq % 4 == 0 && aligned16(lse) && aligned16(dsum);
   hipStream_t s = as_hip(stream);
   const bool split_q = use_split(Lq, B * H), split_k = use_split(Lk, B * H);
   if (split_q && split_k) {
     const dim3 gq16(unsigned((Lq + 15) / 16), unsigned(B * H)), gk16(unsigned((Lk + 15) / 16), unsigned(B * H));
-#define GD_BS1(T, HD, DR, KS)                                                                              \
+#define GD_BS2(T, HD, DR, KS, MK)                                                                          \
   do {                                                                                                     \
-    hipLaunchKernelGGL((attn_bwd_dq_ks_kernel<T, HD, DR, KS>), gq16, dim3(64 * KS), 0, s, a);              \
+    hipLaunchKernelGGL((attn_bwd_dq_ks_kernel<T, HD, DR, KS, MK>), gq16, dim3(64 * KS), 0, s, a);          \
     GD_LAUNCH_CHECK("attn_bwd_dq_ks");                                                                     \
-    hipLaunchKernelGGL((attn_bwd_dkv_qs_kernel<T, HD, DR, KS>), gk16, dim3(64 * KS), 0, s, a);             \
+    hipLaunchKernelGGL((attn_bwd_dkv_qs_kernel<T, HD, DR, KS, MK>), gk16, dim3(64 * KS), 0, s, a);         \
     GD_LAUNCH_CHECK("attn_bwd_dkv_qs");                                                                    \
+  } while (0)
+#define GD_BS1(T, HD, DR, KS)                              \
+  do {                                                     \
+    if (a.mask_kind == 1) GD_BS2(T, HD, DR, KS, 1);        \
+    else if (a.mask_kind == 2) GD_BS2(T, HD, DR, KS, 2);   \
+    else GD_BS2(T, HD, DR, KS, 0);                         \
   } while (0)
 #define GD_BS(T, HD, KS)                     \
   do {                                       \
@@ -226,6 +245,7 @@ extern "C" gd_status gd_attn_backward_dev(gd_dtype dt, int B, int H, int Lq, int
       if (head_dim == 32) GD_BS(float, 32, 2); else GD_BS(float, 64, 2);
     }
 #undef GD_BS1
+#undef GD_BS2
 #undef GD_BS
     return GD_OK;
   }

@@ -110,12 +110,23 @@ bool bwd_regsum() {
   return on;
 }
 
+// the single-pass-softmax backward (wattn_bwd2_kernel) for N <= 64 with a
+// computed index / mask (GD_WATTN_BWD2=0: the round-5 kernel, A/B)
+bool bwd_v2() { return env_int("GD_WATTN_BWD2", 1) != 0; }
+
 template <typename T, int NT, int MODE>
 void launch_bwd_nt(const void* qkv, const void* padv, const WinGeo& geo, const WinCtx& X, const void* out,
                    const void* dout, const float* lse, int B_, void* dqkv, float* grad_pad, float* dtable,
                    hipStream_t s) {
   const int wpb = windows_per_block(B_, X.nH);
   const unsigned nblk = unsigned((B_ + wpb - 1) / wpb) * unsigned(X.nH);
+  if constexpr (NT <= 4 && MODE != kModeAny) {
+    if (bwd_v2()) {
+      hipLaunchKernelGGL((wattn_bwd2_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, (const T*)qkv, (const T*)padv,
+                         geo, X, (const T*)out, (const T*)dout, lse, B_, wpb, (T*)dqkv, grad_pad, dtable);
+      return;
+    }
+  }
   if constexpr (NT <= 4) {
     if (bwd_regsum()) {
       hipLaunchKernelGGL((wattn_bwd_kernel<T, NT, MODE, true>), dim3(nblk), dim3(64 * NT), 0, s, (const T*)qkv,

@@ -63,7 +63,7 @@ def topk_indices(x: Tensor, k: int) -> Tensor:
 
     For slices of >= 20 000 elements PyTorch's topk switches to its
     multi-block radix select, whose captured replay does not follow new
-    input data (tools/probes/graph_topk_probe.py, profiles/r03_graph_topk_probe.log:
+    input data (a round-3 capture probe, profiles/r03_graph_topk_probe.log:
     the replay on new scores returns a different index set than eager).
     S = 22 223 encoder tokens at 800x1333 is above that switch, 6 800 at
     512x640 is below it: the size dependence of the round-2 graph fault.

@@ -113,6 +113,8 @@ inline int __float_as_int(float f) { int v; memcpy(&v, &f, 4); return v; }
 inline float __uint_as_float(unsigned v) { float f; memcpy(&f, &v, 4); return f; }
 inline unsigned __float_as_uint(float f) { unsigned v; memcpy(&v, &f, 4); return v; }
 inline float __expf(float x) { return expf(x); }
+inline float __log2f(float x) { return log2f(x); }
+#define __builtin_amdgcn_exp2f(x) exp2f(x)
 inline int min(int a, int b) { return a < b ? a : b; }
 inline int max(int a, int b) { return a > b ? a : b; }
 

@@ -700,6 +700,31 @@ def test_emulated_attention_wave_tilings(qt, kt, split, monkeypatch):
         assert E.rel_err(mine.double(), r) < 2e-5, name
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
+def test_emulated_attention_growing_logits(dtype, tol):
+    """Logits that grow along the keys by far more than the split forward's
+    lazy-rescale margin (2^8 in p): the reference max moves several times
+    inside one wave's key chunk and the merged states stay exact."""
+    from oracle.blocks import attention_ref
+    g = torch.Generator().manual_seed(5)
+    B, H, Lq, Lk, hd = 1, 2, 40, 700, 32
+    q = torch.randn(B, H, Lq, hd, generator=g).abs()
+    ramp = torch.linspace(0.1, 6.0, Lk)[None, None, :, None]
+    k = (torch.rand(B, H, Lk, hd, generator=g) * ramp)
+    v = torch.randn(B, H, Lk, hd, generator=g)
+    q, k, v = (t.to(dtype) for t in (q, k, v))
+    scale = hd ** -0.5
+    out, lse = E.attn_forward(q, k, v, None, scale)
+    qd, kd, vd = (t.double().requires_grad_(True) for t in (q, k, v))
+    ref = attention_ref(qd, kd, vd, None, scale)
+    assert E.rel_err(out.double(), ref.detach()) < tol
+    grad = torch.randn(B, H, Lq, hd, generator=g).to(dtype)
+    ref.backward(grad.double())
+    dq, dk, dv = E.attn_backward(q, k, v, None, scale, out, lse, grad)
+    for name, mine, r in (("dq", dq, qd.grad), ("dk", dk, kd.grad), ("dv", dv, vd.grad)):
+        assert E.rel_err(mine.double(), r) < tol * 2, name
+
+
 def test_emulated_attention_fully_masked_rows_are_zero():
     """A query row whose keys are all masked gives 0 output and 0 gradients
     (the reference's softmax would give NaN there; no caller produces such

@@ -15,6 +15,25 @@ def _rel(a, b):
     return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
 
 
+# where a bar is the reference's own bf16 floor: the kernel and the reference
+# round the same largest-error element identically in most cases (equal
+# errors to 4 digits, profiles/r06_kernel_margins.jsonl); 1 % of slack on
+# that floor, never on north_star's flat bound
+_FLOOR_SLACK = 1.01
+
+
+def _margin(test, name, err, bar):
+    """Record a measured error against its bar (GD_MARGINS=<path>: one JSON
+    line per check, for profiles/r06*_kernel_margins.jsonl) and assert it."""
+    import json
+    import os
+    path = os.environ.get("GD_MARGINS")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps({"test": test, "check": name, "err": err, "bar": bar, "ok": err < bar}) + "\n")
+    assert err < bar, f"{test} {name}: {err:.3e} >= {bar:.3e}"
+
+
 def _bi_inputs(b, h, s, t, hd, dtype, seed=0, pad=True):
     g = torch.Generator().manual_seed(seed)
     q = torch.randn(b, h, s, hd, generator=g) * hd ** -0.5
@@ -47,8 +66,22 @@ def test_bi_attention_fwd_bwd(dtype, tol, shape):
     dev_in = [x.to(DEV).requires_grad_(True) for x in (q, k, vv, vl)]
     ov, ol = bi_attention_hip(*dev_in, pad_v.to(DEV), pad_l.to(DEV), 0.0)
     ((ov.float() * gv.to(DEV, torch.float32)).sum() + (ol.float() * gl.to(DEV, torch.float32)).sum()).backward()
-    for name, mine, ref in zip(("dq", "dk", "dvv", "dvl"), dev_in, ref_in):
-        assert _rel(mine.grad.cpu(), ref.grad) < tol * 3, name
+    floors = [None] * 4
+    if dtype == torch.bfloat16:
+        # the reference's own bf16 statements (its eager ops under bf16
+        # autocast on the same bf16 inputs) differentiated: their distance
+        # from the fp64 gradients is the floor the reference itself sits at
+        fl_in = [x.float().requires_grad_(True) for x in (q, k, vv, vl)]
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            fv, fl = bi_attention_ref(*fl_in, pad_v, pad_l)
+        ((fv.float() * gv.float()).sum() + (fl.float() * gl.float()).sum()).backward()
+        floors = [_rel(x.grad, r.grad) for x, r in zip(fl_in, ref_in)]
+    for name, mine, ref, fl in zip(("dq", "dk", "dvv", "dvl"), dev_in, ref_in, floors):
+        # north_star's flat bound, or -- where the reference's own bf16
+        # gradient is farther than that from fp64 -- no worse than it
+        check = name if fl is None else f"{name} (ref bf16 floor {fl:.2e})"
+        _margin(f"bi_attention{shape}/{dtype}", check, _rel(mine.grad.cpu(), ref.grad), tol if fl is None else
+                max(tol, _FLOOR_SLACK * fl))
     if dtype == torch.float32:
         assert _rel(ov.cpu(), rv.detach()) < tol
         assert _rel(ol.cpu(), rl.detach()) < tol
@@ -60,9 +93,17 @@ def test_bi_attention_fwd_bwd(dtype, tol, shape):
         # rounding alone reaches ~1.5 % of the largest output against fp64
         with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
             av, al = bi_attention_ref(*[x.float() for x in (q, k, vv, vl)], pad_v, pad_l)
-        assert _rel(ov.cpu(), av.double()) < tol
-        assert _rel(ol.cpu(), al.double()) < tol
-        assert _rel(ov.cpu(), rv.detach()) < 3 * tol and _rel(ol.cpu(), rl.detach()) < 3 * tol
+        t = f"bi_attention{shape}/{dtype}"
+        _margin(t, "out_v_vs_bf16_reference", _rel(ov.cpu(), av.double()), tol)
+        _margin(t, "out_l_vs_bf16_reference", _rel(ol.cpu(), al.double()), tol)
+        # against fp64: the flat 1e-2, or -- where the reference's own bf16
+        # statements are farther than that from fp64 (its measured floor,
+        # computed here) -- no worse than the reference itself
+        floor_v, floor_l = _rel(av.double(), rv.detach()), _rel(al.double(), rl.detach())
+        _margin(t, f"out_v_vs_fp64 (ref bf16 floor {floor_v:.2e})", _rel(ov.cpu(), rv.detach()),
+                max(tol, _FLOOR_SLACK * floor_v))
+        _margin(t, f"out_l_vs_fp64 (ref bf16 floor {floor_l:.2e})", _rel(ol.cpu(), rl.detach()),
+                max(tol, _FLOOR_SLACK * floor_l))
 
 
 def test_bi_attention_production_shape_bf16():
@@ -154,9 +195,10 @@ def test_window_attention_fwd_bwd(dtype, tol, ws, nh, b_, nw, masked):
     out = WindowAttnFunction.apply(qg, tg, ridx.to(DEV), None if mask is None else mask.to(DEV), scale)
     out.backward(grad.to(DEV))
     torch.cuda.synchronize()
-    assert _rel(out.cpu(), ref.detach()) < tol
-    assert _rel(qg.grad.cpu(), qd.grad) < tol * 3
-    assert _rel(tg.grad.cpu(), td.grad) < tol * 3
+    t = f"window_attention{(ws, nh, b_, nw, masked)}/{dtype}"
+    _margin(t, "out", _rel(out.cpu(), ref.detach()), tol)
+    _margin(t, "dqkv", _rel(qg.grad.cpu(), qd.grad), tol)
+    _margin(t, "dtable", _rel(tg.grad.cpu(), td.grad), tol)
 
 
 def test_window_attention_op_dispatch_and_index_paths():
@@ -226,11 +268,12 @@ def test_window_attention_image_fwd_bwd(dtype, tol, b, h, w, ws, shift, nh, bias
     out.backward(grad.to(DEV))
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
-    assert _rel(out.cpu(), ref.detach()) < tol
-    assert _rel(qg.grad.cpu(), qd.grad) < tol * 3
-    assert _rel(tg.grad.cpu(), td.grad) < tol * 3
+    t = f"window_attention_image{(b, h, w, ws, shift, nh, bias)}/{dtype}"
+    _margin(t, "out", _rel(out.cpu(), ref.detach()), tol)
+    _margin(t, "dqkv", _rel(qg.grad.cpu(), qd.grad), tol)
+    _margin(t, "dtable", _rel(tg.grad.cpu(), td.grad), tol)
     if bias:
-        assert _rel(bg.grad.cpu(), bd.grad) < tol * 3
+        _margin(t, "dbias", _rel(bg.grad.cpu(), bd.grad), tol)
 
 
 @pytest.mark.parametrize("standard", [True, False])
@@ -340,9 +383,10 @@ def test_attention_fwd_bwd(dtype, tol, b, h, lq, lk, hd, mask_kind):
     out = AttnFunction.apply(*dev, None if mask is None else mask.to(DEV), scale)
     out.backward(grad.to(DEV))
     torch.cuda.synchronize()
-    assert _rel(out.cpu(), ref.detach()) < tol
+    t = f"attention{(b, h, lq, lk, hd, mask_kind)}/{dtype}"
+    _margin(t, "out", _rel(out.cpu(), ref.detach()), tol)
     for name, mine, r in zip(("dq", "dk", "dv"), dev, ref_in):
-        assert _rel(mine.grad.cpu(), r.grad) < tol * 3, name
+        _margin(t, name, _rel(mine.grad.cpu(), r.grad), tol)
 
 
 def test_attention_op_routes_to_hip_and_falls_back():
@@ -380,9 +424,10 @@ def test_attention_dropout_matches_reference_with_the_kernel_mask(dtype, tol):
     out = AttnFunction.apply(*dev, mask.to(DEV), hd ** -0.5, p, seed_t)
     out.backward(grad.to(DEV))
     torch.cuda.synchronize()
-    assert _rel(out.cpu(), ref.detach()) < tol
+    t = f"attention_dropout/{dtype}"
+    _margin(t, "out", _rel(out.cpu(), ref.detach()), tol)
     for name, mine, r in zip(("dq", "dk", "dv"), dev, ref_in):
-        assert _rel(mine.grad.cpu(), r.grad) < tol * 3, name
+        _margin(t, name, _rel(mine.grad.cpu(), r.grad), tol)
 
 
 def test_attention_dropout_in_a_captured_graph_draws_a_new_mask_per_replay():
@@ -455,8 +500,9 @@ def test_contrastive_logits_and_rowmax(dtype, tol, b, q, t):
     o = out.detach().cpu()
     assert torch.equal(torch.isfinite(o), fin) and (o[~fin] == float("-inf")).all()
     assert _rel(o[fin], ref.detach()[fin]) < tol
-    assert _rel(xg.grad.cpu(), xd.grad) < tol * 3
-    assert _rel(tg.grad.cpu(), td.grad) < tol * 3
+    tn = f"contrastive{(b, q, t)}/{dtype}"
+    _margin(tn, "dx", _rel(xg.grad.cpu(), xd.grad), tol)
+    _margin(tn, "dtext", _rel(tg.grad.cpu(), td.grad), tol)
     rm = contrastive_rowmax_hip(x.to(DEV), text.to(DEV), mask.to(DEV)).cpu()
     assert _rel(rm, ref.detach().max(-1)[0]) < tol
 

@@ -47,6 +47,65 @@ attn)
       --timeout-method thread -k "attention or block" > gpurun_out/attn_tests.log 2>&1 &&
   mfma_pmc attn --cases attn
   ;;
+kern)
+  # attention + window-attention parity on the GPU, then microbench + counters
+  step "pytest attention / window / blocks" &&
+  T 600 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py -m gpu -x -q --timeout 120 \
+      --timeout-method thread -k "attention or block or swin" > gpurun_out/kern_tests.log 2>&1 &&
+  mfma_pmc kern --cases attn,wattn
+  ;;
+margins)
+  # the kernel parity tests with north_star's flat tolerances, every check
+  # recorded (no -x: all margins in one pass), then the MSDA tests
+  step "pytest kernels (margins)"
+  GD_MARGINS=gpurun_out/kernel_margins.jsonl T 900 python3 -u -m pytest tests/test_kernels_gpu.py -m gpu -q \
+      --timeout 120 --timeout-method thread > gpurun_out/margins_tests.log 2>&1
+  rc1=$?
+  [ $rc1 -eq 0 ] || [ $rc1 -eq 1 ] || exit $rc1
+  step "pytest msda" &&
+  T 600 python3 -u -m pytest tests/test_msda_gpu.py -m gpu -q --timeout 120 --timeout-method thread \
+      > gpurun_out/msda_tests.log 2>&1
+  ;;
+km)
+  # margins (all kernel parity checks recorded), MSDA parity, block goldens,
+  # then the attention / window microbench + counters
+  step "pytest kernels (margins)"
+  GD_MARGINS=gpurun_out/kernel_margins.jsonl T 900 python3 -u -m pytest tests/test_kernels_gpu.py -m gpu -q \
+      --timeout 120 --timeout-method thread > gpurun_out/margins_tests.log 2>&1
+  rc1=$?
+  [ $rc1 -eq 0 ] || [ $rc1 -eq 1 ] || exit $rc1
+  step "pytest msda + blocks" &&
+  T 600 python3 -u -m pytest tests/test_msda_gpu.py tests/test_blocks_gpu.py -m gpu -q --timeout 120 \
+      --timeout-method thread > gpurun_out/msda_tests.log 2>&1
+  rc2=$?
+  [ $rc2 -eq 0 ] || [ $rc2 -eq 1 ] || exit $rc2
+  mfma_pmc kern --cases attn,wattn
+  ;;
+km2)
+  # margins + MSDA / block parity, kernel microbench + counters, decoder
+  # MSDA backward variants, the driver's bench command
+  step "pytest kernels (margins)"
+  GD_MARGINS=gpurun_out/kernel_margins.jsonl T 900 python3 -u -m pytest tests/test_kernels_gpu.py -m gpu -q \
+      --timeout 120 --timeout-method thread > gpurun_out/margins_tests.log 2>&1
+  rc1=$?
+  [ $rc1 -eq 0 ] || [ $rc1 -eq 1 ] || exit $rc1
+  step "pytest msda + blocks" &&
+  T 600 python3 -u -m pytest tests/test_msda_gpu.py tests/test_blocks_gpu.py -m gpu -q --timeout 120 \
+      --timeout-method thread > gpurun_out/msda_tests.log 2>&1
+  rc2=$?
+  [ $rc2 -eq 0 ] || [ $rc2 -eq 1 ] || exit $rc2
+  mfma_pmc kern --cases attn,wattn &&
+  step "msda decoder-shape backward variants" &&
+  T 300 python3 tools/msda_microbench.py --bwd-variants --geom dec --variant "lane32,sorted-all,sorted F1,sorted F4" \
+      > gpurun_out/decmsda.jsonl 2>&1 &&
+  step "bench (driver command)" &&
+  T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench.log 2>&1
+  ;;
+decmsda)
+  step "msda decoder-shape backward variants" &&
+  T 300 python3 tools/msda_microbench.py --bwd-variants --geom dec --variant "lane32,sorted-all,sorted F1,sorted F4" \
+      > gpurun_out/decmsda.jsonl 2>&1
+  ;;
 bench)
   step "bench (driver command)" &&
   T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1
