@@ -204,6 +204,180 @@ addln_reduce_kernel(const float* __restrict__ part_w, const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Round 6: the same two kernels with 4 consecutive columns per lane (16-B
+// fp32 / 8-B bf16 vector accesses): lane j owns columns 4j + 256e, e < E4.
+// The one-column-per-lane kernels above issue C/64 scalar 4-B accesses per
+// array and row (256 B per wave instruction) and ran at 1.7-1.9 TB/s in the
+// step (bench hip_entry_points_one_step, round 5); host-checked alignment
+// routes here (GD_ADDLN_V4=0: the scalar kernels, A/B).
+template <typename T> __device__ __forceinline__ void ld4v(const T* p, float v[4]);
+template <> __device__ __forceinline__ void ld4v<float>(const float* p, float v[4]) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+template <> __device__ __forceinline__ void ld4v<uint16_t>(const uint16_t* p, float v[4]) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p);
+  v[0] = bf16_lo(t.x); v[1] = bf16_hi(t.x); v[2] = bf16_lo(t.y); v[3] = bf16_hi(t.y);
+}
+template <typename T> __device__ __forceinline__ void st4v(T* p, const float v[4]);
+template <> __device__ __forceinline__ void st4v<float>(float* p, const float v[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void st4v<uint16_t>(uint16_t* p, const float v[4]) {
+  const uint32_t lo = uint32_t(f32_to_bf16(v[0])) | (uint32_t(f32_to_bf16(v[1])) << 16);
+  const uint32_t hi = uint32_t(f32_to_bf16(v[2])) | (uint32_t(f32_to_bf16(v[3])) << 16);
+  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+}
+
+template <int C>
+__device__ __forceinline__ bool col4_ok(int lane, int e) {
+  return C % 256 == 0 || 4 * lane + 256 * e < C;
+}
+
+template <typename TX, typename TR, int C>
+__global__ void __launch_bounds__(256)
+addln_fwd_v4_kernel(const TX* __restrict__ x, const TR* __restrict__ r, const float* __restrict__ w,
+                    const float* __restrict__ b, int64_t rows, float eps, float* __restrict__ y,
+                    uint16_t* __restrict__ y16, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int E4 = (C + 255) / 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  float wv[E4][4], bv[E4][4];
+#pragma unroll
+  for (int e = 0; e < E4; ++e) {
+    const bool ok = col4_ok<C>(lane, e);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wv[e][i] = ok && w ? w[4 * lane + 256 * e + i] : 1.f;
+      bv[e][i] = ok && b ? b[4 * lane + 256 * e + i] : 0.f;
+    }
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    float s[E4][4];
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      if (col4_ok<C>(lane, e)) {
+        const int64_t o = row * C + 4 * lane + 256 * e;
+        float xv[4], rv[4] = {0.f, 0.f, 0.f, 0.f};
+        ld4v<TX>(x + o, xv);
+        if (r) ld4v<TR>(r + o, rv);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[e][i] = xv[i] + rv[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[e][i] = 0.f;
+      }
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < E4; ++e)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum += s[e][i];
+    const float mean = wsum(sum) / float(C);
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < E4; ++e)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = col4_ok<C>(lane, e) ? s[e][i] - mean : 0.f;
+        sq += d * d;
+      }
+    const float rstd = rsqrtf(wsum(sq) / float(C) + eps);
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      if (!col4_ok<C>(lane, e)) continue;
+      const int64_t o = row * C + 4 * lane + 256 * e;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (s[e][i] - mean) * rstd * wv[e][i] + bv[e][i];
+      st4v<float>(y + o, v);
+      if (y16) st4v<uint16_t>(y16 + o, v);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <typename TX, typename TR, int C>
+__global__ void __launch_bounds__(256)
+addln_bwd_v4_kernel(const float* __restrict__ dy, const float* __restrict__ dy2, const TX* __restrict__ x,
+                    const TR* __restrict__ r, const float* __restrict__ w, const float* __restrict__ mean_in,
+                    const float* __restrict__ rstd_in, int64_t rows, TX* __restrict__ dx, TR* __restrict__ dr,
+                    float* __restrict__ part_w, float* __restrict__ part_b) {
+  constexpr int E4 = (C + 255) / 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_id = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = int64_t(gridDim.x) * 4;
+  float wv[E4][4], gw[E4][4], gb[E4][4];
+#pragma unroll
+  for (int e = 0; e < E4; ++e)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wv[e][i] = col4_ok<C>(lane, e) && w ? w[4 * lane + 256 * e + i] : 1.f;
+      gw[e][i] = gb[e][i] = 0.f;
+    }
+  for (int64_t row = wave_id; row < rows; row += nwaves) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[E4][4], g[E4][4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      const bool ok = col4_ok<C>(lane, e);
+      const int64_t o = row * C + 4 * lane + 256 * e;
+      float xv[4] = {0.f, 0.f, 0.f, 0.f}, rv[4] = {0.f, 0.f, 0.f, 0.f}, d[4] = {0.f, 0.f, 0.f, 0.f},
+            d2[4] = {0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        ld4v<TX>(x + o, xv);
+        if (r) ld4v<TR>(r + o, rv);
+        ld4v<float>(dy + o, d);
+        if (dy2) ld4v<float>(dy2 + o, d2);  // a second consumer's gradient
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xh[e][i] = ok ? (xv[i] + rv[i] - mean) * rstd : 0.f;
+        const float dd = d[i] + d2[i];
+        gw[e][i] += dd * xh[e][i];
+        gb[e][i] += dd;
+        g[e][i] = dd * wv[e][i];
+        sg += g[e][i];
+        sgx += g[e][i] * xh[e][i];
+      }
+    }
+    const float mg = wsum(sg) / float(C), mgx = wsum(sgx) / float(C);
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      if (!col4_ok<C>(lane, e)) continue;
+      const int64_t o = row * C + 4 * lane + 256 * e;
+      float ds[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ds[i] = rstd * (g[e][i] - mg - xh[e][i] * mgx);
+      st4v<TX>(dx + o, ds);
+      if (dr) st4v<TR>(dr + o, ds);
+    }
+  }
+  if (part_w) {  // combine the block's 4 waves in LDS: one partial row per block
+    __shared__ float red[2][4][C];
+    const int wv_i = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      if (!col4_ok<C>(lane, e)) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[0][wv_i][4 * lane + 256 * e + i] = gw[e][i];
+        red[1][wv_i][4 * lane + 256 * e + i] = gb[e][i];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      part_w[int64_t(blockIdx.x) * C + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+      part_b[int64_t(blockIdx.x) * C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Three-input variant for the deformable layers' attention sublayer (C = 256):
 //   y = LayerNorm(x + (r + drop(r2)))
 // x the fp32 residual stream, r the fp32 identity the MSDA module adds
@@ -495,6 +669,13 @@ Drop3 make_drop3(float p, uint32_t seed, const uint32_t* seed_dev) {
 
 constexpr int kLnBlocks = 512;  // backward grid: 2048 waves, one partial row per block
 
+// the 4-column vector kernels: a null pointer or one aligned to its 4-element
+// vector (16 B fp32, 8 B bf16); GD_ADDLN_V4=0 keeps the scalar kernels (A/B)
+bool v4_ok(const void* p, gd_dtype dt) {
+  if (env_int("GD_ADDLN_V4", 1) == 0) return false;
+  return !p || (reinterpret_cast<uintptr_t>(p) & (dt == GD_BF16 ? 7 : 15)) == 0;
+}
+
 template <typename Fn>
 gd_status dispatch_types(gd_dtype tx, gd_dtype tr, bool has_r, int C, Fn&& fn) {
   GD_REQUIRE(tx == GD_F32 || tx == GD_BF16, "add_layernorm: x dtype %d (F32, BF16)", int(tx));
@@ -551,11 +732,16 @@ extern "C" gd_status gd_add_layernorm_forward2(gd_dtype x_dtype, const void* x, 
   hipStream_t s = as_hip(stream);
   const int64_t blocks64 = (rows + 3) / 4;
   const unsigned blocks = unsigned(blocks64 < 8192 ? blocks64 : 8192);
+  const bool v4 = v4_ok(x, x_dtype) && v4_ok(r, r_dtype) && v4_ok(y, GD_F32) && v4_ok(y_bf16, GD_BF16);
   gd_status st = dispatch_types(x_dtype, r_dtype, r != nullptr, C, [&](auto tx, auto tr, auto e) {
     using TX = decltype(tx);
     using TR = decltype(tr);
-    hipLaunchKernelGGL((addln_fwd_kernel<TX, TR, decltype(e)::value>), dim3(blocks), dim3(256), 0, s,
-                       (const TX*)x, (const TR*)r, weight, bias, rows, eps, y, (uint16_t*)y_bf16, mean, rstd);
+    if (v4)
+      hipLaunchKernelGGL((addln_fwd_v4_kernel<TX, TR, decltype(e)::value>), dim3(blocks), dim3(256), 0, s,
+                         (const TX*)x, (const TR*)r, weight, bias, rows, eps, y, (uint16_t*)y_bf16, mean, rstd);
+    else
+      hipLaunchKernelGGL((addln_fwd_kernel<TX, TR, decltype(e)::value>), dim3(blocks), dim3(256), 0, s,
+                         (const TX*)x, (const TR*)r, weight, bias, rows, eps, y, (uint16_t*)y_bf16, mean, rstd);
   });
   if (st != GD_OK) return st;
   GD_LAUNCH_CHECK("add_layernorm_fwd");
@@ -597,12 +783,19 @@ extern "C" gd_status gd_add_layernorm_backward2(gd_dtype x_dtype, const void* x,
   hipStream_t s = as_hip(stream);
   float* part_w = grad_weight ? static_cast<float*>(workspace) : nullptr;
   float* part_b = grad_weight ? part_w + int64_t(kLnBlocks) * C : nullptr;
+  const bool v4 = v4_ok(x, x_dtype) && v4_ok(r, r_dtype) && v4_ok(grad_y, GD_F32) && v4_ok(grad_y2, GD_F32) &&
+                  v4_ok(grad_x, x_dtype) && v4_ok(grad_r, r_dtype);
   gd_status st = dispatch_types(x_dtype, r_dtype, r != nullptr, C, [&](auto tx, auto tr, auto e) {
     using TX = decltype(tx);
     using TR = decltype(tr);
-    hipLaunchKernelGGL((addln_bwd_kernel<TX, TR, decltype(e)::value>), dim3(kLnBlocks), dim3(256), 0, s, grad_y,
-                       grad_y2, (const TX*)x, (const TR*)r, weight, mean, rstd, rows, (TX*)grad_x, (TR*)grad_r, part_w,
-                       part_b);
+    if (v4)
+      hipLaunchKernelGGL((addln_bwd_v4_kernel<TX, TR, decltype(e)::value>), dim3(kLnBlocks), dim3(256), 0, s,
+                         grad_y, grad_y2, (const TX*)x, (const TR*)r, weight, mean, rstd, rows, (TX*)grad_x,
+                         (TR*)grad_r, part_w, part_b);
+    else
+      hipLaunchKernelGGL((addln_bwd_kernel<TX, TR, decltype(e)::value>), dim3(kLnBlocks), dim3(256), 0, s, grad_y,
+                         grad_y2, (const TX*)x, (const TR*)r, weight, mean, rstd, rows, (TX*)grad_x, (TR*)grad_r,
+                         part_w, part_b);
   });
   if (st != GD_OK) return st;
   GD_LAUNCH_CHECK("add_layernorm_bwd");

@@ -48,10 +48,15 @@ gd_status check(gd_dtype dt, const void* qkv, const float* table, const int64_t*
   return GD_OK;
 }
 
-// windows per block: about 2048 blocks over the whole launch, at most 8
+// windows per block: about GD_WATTN_BLOCKS workgroups over the launch
+// (default 1024: 3-4 resident per CU, so every block runs several windows
+// with the next one's loads in flight -- at 2048 the later Swin stages got
+// one window per block, whose loads and prologue nothing overlapped), at
+// most 8
 int windows_per_block(int B_, int nH) {
   const int64_t tasks = int64_t(B_) * nH;
-  return int(std::max<int64_t>(1, std::min<int64_t>(8, tasks / 2048)));
+  const int64_t target = std::max(64, env_int("GD_WATTN_BLOCKS", 1024));
+  return int(std::max<int64_t>(1, std::min<int64_t>(8, (tasks + target - 1) / target)));
 }
 
 WinCtx make_ctx(const float* table, const int64_t* ridx, const float* mask, int N, int nH, int nW, int ws,

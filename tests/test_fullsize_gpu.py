@@ -82,13 +82,17 @@ MARGINS = "gpurun_out/fullsize_margins.jsonl"
 
 def _record_margins(test, rows):
     """Keep every compared output's P / C error (appended as one JSON line per
-    test; the GPU session copies the file to profiles/)."""
+    test; the GPU session copies the file to profiles/): P_vs_F is the
+    product's error against the fp32 reference composition, C_vs_F the
+    reference composition's own bf16 error, next to north_star's flat verdict
+    (flat_ok) and the relaxed one the assertion uses (rule_ok)."""
     import json
     import os
     os.makedirs(os.path.dirname(MARGINS), exist_ok=True)
     with open(MARGINS, "a") as f:
         f.write(json.dumps({"test": test, "tol": TOL, "bf16_ratio": BF16_RATIO,
-                            "rows": [{"name": n, "P": p, "C": c, "flat_ok": p <= TOL,
+                            "rows": [{"name": n, "P": p, "C": c, "P_vs_F": p, "C_vs_F": c,
+                                      "P_below_C": p <= c, "flat_ok": p <= TOL,
                                       "rule_ok": p <= max(TOL, BF16_RATIO * c)} for n, p, c in rows]}) + "\n")
 
 

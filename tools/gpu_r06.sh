@@ -101,6 +101,23 @@ km2)
   step "bench (driver command)" &&
   T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench.log 2>&1
   ;;
+r6d)
+  # add+LayerNorm vector kernels and the window-attention block heuristic:
+  # parity, window microbench A/B, the driver's bench, kernel census trace
+  step "pytest norm / window / blocks / stepgraph" &&
+  T 900 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py tests/test_stepgraph_gpu.py -m gpu -q \
+      --timeout 120 --timeout-method thread -k "norm or window or block or swin or step" > gpurun_out/r6d_tests.log 2>&1 &&
+  step "wattn microbench (blocks 1024 / 2048)" &&
+  T 300 python3 tools/attn_microbench.py --cases wattn > gpurun_out/r6d_wattn_1024.jsonl 2>&1 &&
+  GD_WATTN_BLOCKS=2048 T 300 python3 tools/attn_microbench.py --cases wattn > gpurun_out/r6d_wattn_2048.jsonl 2>&1 &&
+  step "bench (driver command)" &&
+  T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r6d_bench.log 2>&1 &&
+  step "census trace" &&
+  T 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/r6d_prof" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 4 --warmup 3 --ckpt-compare off > gpurun_out/r6d_prof.log 2>&1 &&
+  kt=$(find "$PROF/r6d_prof" -name '*kernel_trace.csv' | head -n 1) &&
+  python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/r6d_steady_state.txt 2>&1
+  ;;
 decmsda)
   step "msda decoder-shape backward variants" &&
   T 300 python3 tools/msda_microbench.py --bwd-variants --geom dec --variant "lane32,sorted-all,sorted F1,sorted F4" \

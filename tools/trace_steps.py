@@ -74,6 +74,26 @@ def main():
     for (k, gx, gy), (n, us) in sorted(gd.items(), key=lambda kv: -kv[1][1]):
         print(f"  {k:45s} grid=({gx},{gy}) launches/step={n / nsteps:5.1f} avg={us / n:9.1f}us "
               f"total={us / nsteps / 1e3:7.2f} ms/step")
+    # one replayed graph step: the interval between two optimizer chains
+    # whose kernel count is the most common one (the capture step and the
+    # eager per-entry-point step have other counts)
+    ivs = [(bounds[i] + 1, bounds[i + 1] + 1) for i in range(len(bounds) - 1)]
+    if ivs:
+        counts = collections.Counter(b - a for a, b in ivs)
+        mode = counts.most_common(1)[0][0]
+        a0, b0 = [iv for iv in ivs if iv[1] - iv[0] == mode][-1]
+        one = rows[a0:b0]
+        busy1 = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in one)
+        wall1 = (int(one[-1]["End_Timestamp"]) - int(one[0]["Start_Timestamp"])) / 1e6
+        print(f"--- one graph step (kernel indices {a0}..{b0}, {counts[mode]} steps of this count): "
+              f"kernels {len(one)} busy {busy1:.2f} ms wall {wall1:.2f} ms")
+        g1 = collections.defaultdict(lambda: [0, 0.0])
+        for r in one:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            g1[re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))[:90]][0] += 1
+            g1[re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))[:90]][1] += d
+        for k, (n, us) in sorted(g1.items(), key=lambda kv: -kv[1][1])[:60]:
+            print(f"  {us:9.1f} us n={n:4d} avg={us / n:7.1f}  {k}")
     print("--- top individual kernels")
     for k, (n, ms) in sorted(by_full.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"  {ms / nsteps:8.2f} ms/step  n/step={n / nsteps:6.1f} avg={ms / n * 1e3:8.1f}us  {k}")
