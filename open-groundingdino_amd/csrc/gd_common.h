@@ -151,6 +151,33 @@ __device__ __forceinline__ void lds_dma16(const void* src, void* dst) {
     __builtin_amdgcn_s_barrier();             \
     __asm__ __volatile__("" ::: "memory");    \
   } while (0)
+// An opaque copy of a per-lane integer: values derived from the copy cannot
+// be computed once and kept live in registers from an earlier use of the
+// original (a register-pressure valve for kernel epilogues)
+#ifndef gd_opaque_i32
+namespace {
+__device__ __forceinline__ int gd_opaque_i32(int x) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+}  // namespace
+#endif
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and
+// scalar-memory) operations, then s_barrier -- NOT for its global loads and
+// stores.  __syncthreads() waits vmcnt(0) as well, so a barrier inside a
+// loop that prefetches the next iteration's global data (or has issued
+// global stores) exposes their whole latency at every barrier.
+#ifndef gd_lds_barrier
+#define gd_lds_barrier()                                                     \
+  do {                                                                       \
+    __asm__ __volatile__("" ::: "memory");                                   \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0), vmcnt / expcnt open */ \
+    __builtin_amdgcn_s_barrier();                                            \
+    __asm__ __volatile__("" ::: "memory");                                   \
+  } while (0)
+#endif
+
 // Wave-level ordering point for wave-private LDS: the wave runs in lock step
 // and a wave's LDS instructions execute in order, so a ds_write by one lane
 // is visible to a later ds_read by another lane of the same wave; this only

@@ -412,6 +412,7 @@ inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 #define __builtin_amdgcn_s_barrier() ::gd_emu::syncthreads()
 #define gd_wave_sync() ::gd_emu::wave_sync()
 #define __builtin_amdgcn_s_waitcnt(imm) ((void)(imm))  // memory is synchronous here
+#define gd_opaque_i32(x) (x)  // gd_common.h: a register-allocation hint only
 #define GD_LDS_DMA16(src, dst) ::gd_emu::lds_dma16((const void*)(src), (void*)(dst))
 // compiler scheduling hints: no semantics to emulate
 #define __builtin_amdgcn_sched_barrier(mask) ((void)(mask))

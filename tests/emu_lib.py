@@ -25,7 +25,7 @@ def lib():
         # GD_EMU_ASAN=1: the AddressSanitizer build (the process must preload
         # the clang ASan runtime; see tests/test_emu_kernels.py)
         asan = os.environ.get("GD_EMU_ASAN") == "1"
-        subprocess.run(["make", "-s", "-C", EMU_DIR] + (["asan"] if asan else []), check=True)
+        subprocess.run(["make", "-s", "-j8", "-C", EMU_DIR] + (["asan"] if asan else []), check=True)
         _LIB = ctypes.CDLL(os.path.join(EMU_DIR, "_build", "libgd_emu_asan.so" if asan else "libgd_emu.so"))
         _LIB.gd_msda_forward.argtypes = [_i, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p]
         _LIB.gd_msda_backward.argtypes = [_i, _p, _p, _p, _p, _p, _p] + [_i] * 7 + [_p, _p, _p, _p]

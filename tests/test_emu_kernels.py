@@ -495,7 +495,7 @@ def test_emulated_kernels_under_address_sanitizer():
         pytest.skip("clang ASan runtime not available")
     paths = [HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "open-groundingdino_amd")]
     env = dict(os.environ, GD_EMU_ASAN="1", LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0", OMP_NUM_THREADS="1")
-    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "emu"), "asan"], check=True)
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(HERE, "emu"), "asan"], check=True)
     procs = [subprocess.Popen([sys.executable, "-c", _ASAN_HEAD.format(paths=paths) + g + 'print("asan-clean")'],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
              for g in _ASAN_GROUPS]

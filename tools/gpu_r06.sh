@@ -118,6 +118,31 @@ r6d)
   kt=$(find "$PROF/r6d_prof" -name '*kernel_trace.csv' | head -n 1) &&
   python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/r6d_steady_state.txt 2>&1
   ;;
+r6e)
+  # window attention with LDS-only in-loop barriers: parity, microbench,
+  # then the census (below)
+  step "pytest window / blocks" &&
+  T 900 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py -m gpu -q \
+      --timeout 120 --timeout-method thread -k "window or block or swin" > gpurun_out/r6e_tests.log 2>&1 &&
+  step "wattn microbench" &&
+  T 300 python3 tools/attn_microbench.py --cases wattn > gpurun_out/r6e_wattn.jsonl 2>&1 &&
+  step "census trace" &&
+  T 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/census" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 4 --warmup 3 --ckpt-compare off > gpurun_out/census_prof.log 2>&1 &&
+  kt=$(find "$PROF/census" -name '*kernel_trace.csv' | head -n 1) &&
+  python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/census_steady_state.txt 2>&1 &&
+  step "glue census (all ops)" &&
+  T 300 python3 tools/glue_census.py --min-numel 1 --out gpurun_out/census_glue_all.txt > gpurun_out/census_glue.log 2>&1
+  ;;
+census)
+  step "census trace" &&
+  T 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/census" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 4 --warmup 3 --ckpt-compare off > gpurun_out/census_prof.log 2>&1 &&
+  kt=$(find "$PROF/census" -name '*kernel_trace.csv' | head -n 1) &&
+  python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/census_steady_state.txt 2>&1 &&
+  step "glue census (all ops)" &&
+  T 300 python3 tools/glue_census.py --min-numel 1 --out gpurun_out/census_glue_all.txt > gpurun_out/census_glue.log 2>&1
+  ;;
 decmsda)
   step "msda decoder-shape backward variants" &&
   T 300 python3 tools/msda_microbench.py --bwd-variants --geom dec --variant "lane32,sorted-all,sorted F1,sorted F4" \
