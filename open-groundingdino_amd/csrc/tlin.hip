@@ -135,26 +135,41 @@ tlin_fwd_kernel(const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __r
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = wmma(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = wmma(bf[j], af[i], acc[i][j]);
     }
   }
 
-  // epilogue: acc[i][j][r] = y[m0 + 64 wm + 16 i + 4 g + r][n0 + 64 wn + 16 j + c]
+  // epilogue: the product is accumulated transposed (W rows as the MFMA's A
+  // operand), acc[i][j][r] = y[m0 + 64 wm + 16 i + c][n0 + 64 wn + 16 j + 4 g + r]:
+  // a lane's 4 values are consecutive outputs of one token, packed to one
+  // 8-B ds_write (16 per lane instead of 64 2-B writes, whose bank conflicts
+  // were 30 % of the LDS cycles at the encoder FFN shape; a 16-lane group
+  // of one write covers 16 rows at dword offset 4c: conflict-free)
   __syncthreads();  // every wave's last fragment reads are done
   uint16_t* ot = lds;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = 64 * wn + 16 * j + c;
-    float bv = 0.f;
-    if (BIAS && n0 + col < N) bv = bf16_to_f32(bias[n0 + col]);
+    const int col = 64 * wn + 16 * j + 4 * g;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (BIAS && n0 + col < N) {
+      const uint2 b2 = *reinterpret_cast<const uint2*>(bias + n0 + col);
+      bv[0] = __uint_as_float(b2.x << 16);
+      bv[1] = __uint_as_float(b2.x & 0xffff0000u);
+      bv[2] = __uint_as_float(b2.y << 16);
+      bv[3] = __uint_as_float(b2.y & 0xffff0000u);
+    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = acc[i][j][r] + bv;
-        if (RELU) v = v > 0.f ? v : 0.f;
-        ot[(64 * wm + 16 * i + 4 * g + r) * kTlOutPitch + col] = f32_to_bf16(v);
+        v[r] = acc[i][j][r] + bv[r];
+        if (RELU) v[r] = v[r] > 0.f ? v[r] : 0.f;
       }
+      *reinterpret_cast<uint2*>(ot + (64 * wm + 16 * i + c) * kTlOutPitch + col) =
+          make_uint2(uint32_t(f32_to_bf16(v[0])) | (uint32_t(f32_to_bf16(v[1])) << 16),
+                     uint32_t(f32_to_bf16(v[2])) | (uint32_t(f32_to_bf16(v[3])) << 16));
+    }
   }
   __syncthreads();
   // 128 rows x 16 vectors of 8 outputs; 16 lanes per row
@@ -191,6 +206,7 @@ extern "C" gd_status gd_token_linear_forward(const void* x, int64_t ldx, const v
              "token_linear: M=%d K=%d N=%d (K, N multiples of 8)", M, K, N);
   if (M == 0) return GD_OK;
   GD_REQUIRE(x && weight && y, "token_linear: null pointer");
+  GD_REQUIRE(!bias || (reinterpret_cast<uintptr_t>(bias) & 7) == 0, "token_linear: bias must be 8-byte aligned");
   GD_REQUIRE(aligned16(x) && aligned16(weight) && aligned16(y) && ldx % 8 == 0 && ldy % 8 == 0 && ldx >= K &&
                  ldy >= N,
              "token_linear: 16-byte aligned rows required (ldx=%lld ldy=%lld)", (long long)ldx, (long long)ldy);

@@ -53,11 +53,15 @@ TLIN_MIN_TOKENS = 2048
 
 
 def tlin_wins(k: int, n: int) -> bool:
-    """The shapes where the kernel beats the library GEMM
-    (profiles/r05m_gemm_shapes.jsonl): a narrow reduction or output (Swin-T
-    stage 0's K = 96 / N = 96: 40 vs 69 us, 33 vs 55 us); at K, N >= 256 the
-    library's tiles are faster (18 vs 14 us at 256 -> 256)."""
-    return min(k, n) <= TLIN_MAX_NARROW
+    """The shapes where the kernel beats the library GEMM, device time from
+    graph replays (tools/tlin_microbench.py, profiles/r06f_tlin_shapes.jsonl):
+    a narrow reduction (Swin-T stage 0, K = 96: 41 vs 69 us at 96 -> 288,
+    19 vs 34 at 96 -> 96) or output (stage 0's fc2, N = 96), and the wide
+    expansions of the 192- / 384-channel stages (192 -> 576: 25 vs 29 us,
+    192 -> 768: 30 vs 36, 384 -> 1152: 21 vs 25).  Everywhere else the
+    library's tiles are faster (K = 256: 18 vs 14 us at 256 -> 256, 54 vs
+    45 at 256 -> 1024; square 192 / 384 shapes; K >= 768)."""
+    return k <= TLIN_MAX_NARROW or n <= 96 or (k in (192, 384) and n >= 3 * k)
 
 
 TLIN_MAX_NARROW = 128
@@ -70,7 +74,8 @@ def tlin_ok(x2: torch.Tensor, wc: torch.Tensor, bc) -> bool:
     n = wc.shape[0]
     return (TLIN and _lib.enabled("tlin") and _lib.on_device(x2) and m >= TLIN_MIN_TOKENS and tlin_wins(k, n)
             and x2.dtype == wc.dtype == torch.bfloat16 and (bc is None or (bc.dtype == torch.bfloat16
-                                                                           and bc.is_contiguous()))
+                                                                           and bc.is_contiguous()
+                                                                           and bc.data_ptr() % 8 == 0))
             and wc.is_contiguous() and k % 8 == 0 and n % 8 == 0 and x2.stride(1) == 1 and x2.stride(0) % 8 == 0
             and x2.data_ptr() % 16 == 0 and wc.data_ptr() % 16 == 0)
 

@@ -1116,6 +1116,13 @@ def test_emulated_query_anchors(transposed, monkeypatch):
     (257, 96, 288, True, True, 0),       # Swin-T stage 0: K = 96 (half chunk), N = 288 (partial N tile)
     (130, 384, 96, False, False, 8),     # no bias, x rows padded (ldx = K + 8)
     (64, 2048, 136, True, True, 0),      # long K, N = 136 (one full and one 8-wide N tile)
+    # the x-resident kernel (K <= 256): K = 192 with padded rows, K = 128
+    # with a 40-wide last column block, K = 88 (zero-filled K tail of the
+    # 96-wide tile), and a column split over workgroups (few token tiles)
+    (200, 192, 576, False, True, 8),
+    (77, 128, 40, True, False, 0),
+    (150, 88, 64, False, True, 0),
+    (40, 256, 1024, True, True, 0),
 ])
 def test_emulated_token_linear_forward(m, k, n, relu, bias, pad):
     """csrc/tlin.hip y = x W^T (+ b) (ReLU), bf16 in / out, fp32 accumulate,
@@ -1139,7 +1146,7 @@ def test_emulated_token_linear_forward(m, k, n, relu, bias, pad):
     assert bool(((y.double() - ref).abs() <= ulp).all()), float(((y.double() - ref).abs() / ulp).max())
 
 
-@pytest.mark.parametrize("m,k,n,pad", [(300, 256, 2048, 0), (130, 64, 136, 8)])
+@pytest.mark.parametrize("m,k,n,pad", [(300, 256, 2048, 0), (130, 64, 136, 8), (100, 192, 264, 8)])
 def test_emulated_token_linear_forward_masked(m, k, n, pad):
     """gd_token_linear_forward_masked: the bf16 product where the mask is
     > 0, +0 elsewhere (threshold_backward on the rounded product: negative,

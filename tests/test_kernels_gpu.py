@@ -842,7 +842,8 @@ def test_box_refine_matches_composition(dd, monkeypatch):
     assert _rel(got[2], want[2]) < 1e-5
 
 
-@pytest.mark.parametrize("m,k,n", [(44446, 256, 2048), (2048 + 40, 256, 136)])
+@pytest.mark.parametrize("m,k,n", [(44446, 256, 2048), (2048 + 40, 256, 136), (133600, 96, 288), (33400, 192, 576),
+                                   (44446, 384, 256)])
 def test_token_linear_forward_and_masked_dx(m, k, n):
     """csrc/tlin.hip at the encoder FFN shape: the relu forward
     (y = relu(x W1^T + b1)) and the masked input gradient of the second

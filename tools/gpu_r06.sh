@@ -134,6 +134,61 @@ r6e)
   step "glue census (all ops)" &&
   T 300 python3 tools/glue_census.py --min-numel 1 --out gpurun_out/census_glue_all.txt > gpurun_out/census_glue.log 2>&1
   ;;
+tlx)
+  # x-resident token-linear kernel: parity, then shapes A/B against the
+  # chunked kernel and the library GEMM
+  step "pytest token linear / blocks" &&
+  T 600 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_blocks_gpu.py -m gpu -q --timeout 120 \
+      --timeout-method thread -k "linear or tlin or block or ffn" > gpurun_out/tlx_tests.log 2>&1 &&
+  step "tlin microbench" &&
+  T 300 python3 tools/tlin_microbench.py > gpurun_out/tlx_mb.jsonl 2>&1
+  ;;
+fin)
+  # the round's final evidence: the whole GPU suite (kernel margins recorded),
+  # smoke, microbenchmarks, the driver's bench, then the rocprofv3 trace and
+  # the FETCH_SIZE / WRITE_SIZE passes of the same step (one counter per run)
+  step "pytest -m gpu (margins recorded)"
+  GD_MARGINS=gpurun_out/fin_kernel_margins.jsonl T 600 python3 -u -m pytest tests -m gpu -q --timeout 120 \
+      --timeout-method thread > gpurun_out/fin_gpu_tests.log 2>&1
+  rc1=$?
+  [ $rc1 -eq 0 ] || [ $rc1 -eq 1 ] || exit $rc1
+  step "smoke" &&
+  T 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/fin_smoke.log 2>&1 &&
+  step "microbenchmarks" &&
+  T 200 python3 tools/tlin_microbench.py > gpurun_out/fin_tlin.jsonl 2>&1 &&
+  T 200 python3 tools/attn_microbench.py --cases attn,wattn > gpurun_out/fin_attn_mb.jsonl 2>&1 &&
+  step "bench (driver command)" &&
+  T 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/fin_bench.log 2>&1 &&
+  step "rocprof kernel trace" &&
+  T 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/fin_prof" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 4 --warmup 3 --ckpt-compare off > gpurun_out/fin_prof.log 2>&1 &&
+  mkdir -p gpurun_out/fin_prof &&
+  find "$PROF/fin_prof" -name '*stats*.csv' -exec cp {} gpurun_out/fin_prof/ \; &&
+  kt=$(find "$PROF/fin_prof" -name '*kernel_trace.csv' | head -n 1) &&
+  python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/fin_prof/steady_state.txt 2>&1 &&
+  step "pmc FETCH_SIZE" &&
+  T 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$PROF/fin_fetch" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --ckpt-compare off > gpurun_out/fin_fetch.log 2>&1 &&
+  step "pmc WRITE_SIZE" &&
+  T 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$PROF/fin_write" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --ckpt-compare off > gpurun_out/fin_write.log 2>&1 &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/fin_fetch" --write "$PROF/fin_write" \
+      --out gpurun_out/fin_pmc_traffic.json > gpurun_out/fin_pmc_traffic.log 2>&1 &&
+  exit $rc1
+  ;;
+lossab)
+  # which round-6 kernel change moved cfg3's bf16 loss error: the full-size
+  # gradient test under each A/B switch (one process per setting)
+  for sw in BASE GD_ATTN_SPLIT=0 GD_WATTN_BWD2=0 GD_ADDLN_V4=0 GD_TLIN=0; do
+    step "cfg3 with $sw"
+    if [ "$sw" = BASE ]; then e=(); else e=("$sw"); fi
+    env "${e[@]}" timeout -k 10 300 python3 -u -m pytest tests/test_fullsize_gpu.py -m gpu -q -s --timeout 240 \
+        --timeout-method thread -k cfg3_gradients > "gpurun_out/lossab_${sw%%=*}.log" 2>&1
+    rc=$?
+    [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+    grep -E "loss:|pred_logits:|q0.5" "gpurun_out/lossab_${sw%%=*}.log"
+  done
+  ;;
 census)
   step "census trace" &&
   T 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/census" -o run -- \
