@@ -417,6 +417,7 @@ class _AddScaled(torch.autograd.Function):
                           out.data_ptr(), _lib.stream_of(x),
                           nbytes=x.numel() * (xc.element_size() + bc.element_size() + out.element_size()))
                 ctx.kernel = True
+                ctx.lay = lay  # the backward reuses the fp32 scale (no second cast kernel)
                 return out
         ctx.kernel = False
         with torch.autocast(device_type=x.device.type, enabled=False):
@@ -452,7 +453,7 @@ class _AddScaled(torch.autograd.Function):
     def _backward_kernel(ctx, g, branch, s):
         shape, dtype = ctx.branch_meta
         bsz, n, c = shape
-        s32, sbs, scs = _scale_layout(g, s)
+        s32, sbs, scs = ctx.lay
         g = g.contiguous()
         if g.dtype not in (torch.float32, torch.bfloat16):
             g = g.float()

@@ -181,8 +181,11 @@ class WindowAttnImageFunction(torch.autograd.Function):
         nh = table32.shape[1]
         dout = dout.to(qkv.dtype).contiguous()
         dqkv = torch.empty_like(qkv)
-        dbias = None if bias is None else torch.zeros(c3, dtype=torch.float32, device=qkv.device)
-        dtable = torch.zeros_like(table32)
+        # the two atomically accumulated gradients zeroed by ONE fill kernel
+        nb = 0 if bias is None else c3
+        zbuf = torch.zeros(nb + table32.numel(), dtype=torch.float32, device=qkv.device)
+        dbias = None if bias is None else zbuf[:c3]
+        dtable = zbuf[nb:].view(table32.shape)
         _lib.call("gd_window_attn_image_backward", _lib.dtype_code(qkv), qkv.data_ptr(), _lib.ptr(bias),
                   table32.data_ptr(), _lib.ptr(ridx), _lib.ptr(mask32), out.data_ptr(), dout.data_ptr(),
                   lse.data_ptr(), b, hw[0], hw[1], ws, shift, nh, c3 // (3 * nh), scale, dqkv.data_ptr(),

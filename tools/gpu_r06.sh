@@ -176,6 +176,22 @@ fin)
       --out gpurun_out/fin_pmc_traffic.json > gpurun_out/fin_pmc_traffic.log 2>&1 &&
   exit $rc1
   ;;
+fin2)
+  # after the last host-side launch trims: the GPU suite, the driver's bench
+  # and the graph-step census
+  step "pytest -m gpu"
+  T 600 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/fin2_gpu_tests.log 2>&1
+  rc1=$?
+  [ $rc1 -eq 0 ] || [ $rc1 -eq 1 ] || exit $rc1
+  step "bench (driver command)" &&
+  T 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/fin2_bench.log 2>&1 &&
+  step "census trace" &&
+  T 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/fin2" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 4 --warmup 3 --ckpt-compare off > gpurun_out/fin2_prof.log 2>&1 &&
+  kt=$(find "$PROF/fin2" -name '*kernel_trace.csv' | head -n 1) &&
+  python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/fin2_steady_state.txt 2>&1 &&
+  exit $rc1
+  ;;
 lossab)
   # which round-6 kernel change moved cfg3's bf16 loss error: the full-size
   # gradient test under each A/B switch (one process per setting)
