@@ -18,6 +18,7 @@ from torch import Tensor, nn
 
 from . import castcache
 from .misc import inverted, mask_cache_key, split_last
+from .wgrad import _dx
 
 
 def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor], b: int, h: int,
@@ -57,6 +58,17 @@ def merge_masks(attn_mask: Optional[Tensor], key_padding_mask: Optional[Tensor],
 PACKED_INPROJ = True
 
 
+def _low(x, dt):
+    """x in dtype dt: the bf16 twin written beside x by its producer when it
+    is current (misc.add_with_twins, layernorm), else a cast."""
+    if x.dtype == dt:
+        return x
+    tw = getattr(x, "_gd_bf16", None)
+    if tw is not None and tw[1] == x._version and tw[0].dtype == dt and tw[0].shape == x.shape:
+        return tw[0]
+    return x.to(dt)
+
+
 class _PackedInProj(torch.autograd.Function):
     """Two row blocks of a packed projection: ya = xa W[:split]^T + b[:split],
     yb = xb W[split:]^T + b[split:].  Same GEMMs as two F.linear calls on
@@ -65,6 +77,13 @@ class _PackedInProj(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, w, b, xa, xb, split):
+        # xa / xb in their own dtype (the decoder's fp32 stream): the
+        # low-precision copy is the bf16 twin a producer wrote beside the
+        # tensor (misc.add_with_twins) or a cast here, and the backward
+        # writes dX in x's dtype straight from the GEMM (wgrad._dx) -- no
+        # cast kernel and no ToCopy backward per input
+        ctx.x_dtypes = (xa.dtype, xb.dtype)
+        xa, xb = _low(xa, w.dtype), _low(xb, w.dtype)
         ctx.save_for_backward(w, xa, xb)
         ctx.split = split
         return castcache.linear2d(xa, w[:split], b[:split]), castcache.linear2d(xb, w[split:], b[split:])
@@ -79,8 +98,8 @@ class _PackedInProj(torch.autograd.Function):
         if dyb is None:
             dyb = torch.zeros(*xb.shape[:-1], w.shape[0] - sp, dtype=w.dtype, device=w.device)
         ga, gb = dya.reshape(-1, sp), dyb.reshape(-1, w.shape[0] - sp)
-        dxa = (ga @ w[:sp]).view(xa.shape) if ctx.needs_input_grad[2] else None
-        dxb = (gb @ w[sp:]).view(xb.shape) if ctx.needs_input_grad[3] else None
+        dxa = _dx(ga, w[:sp], ctx.x_dtypes[0]).view(xa.shape) if ctx.needs_input_grad[2] else None
+        dxb = _dx(gb, w[sp:], ctx.x_dtypes[1]).view(xb.shape) if ctx.needs_input_grad[3] else None
         dw = db = None
         if ctx.needs_input_grad[0]:
             dw = torch.empty_like(w)
@@ -132,7 +151,7 @@ class MultiheadAttention(nn.Module):
             if bias is not None and PACKED_INPROJ and (query is key or key is value):
                 split = 2 * e if query is key else e
                 xa, xb = (query, value) if query is key else (query, key)
-                ya, yb = _PackedInProj.apply(w, bias, xa.to(dt), xb.to(dt), split)
+                ya, yb = _PackedInProj.apply(w, bias, xa, xb, split)
                 if query is key:
                     q, k = split_last(ya, (e, e))
                     return q, k, yb

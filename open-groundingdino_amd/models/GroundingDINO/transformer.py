@@ -527,7 +527,10 @@ class DeformableTransformerDecoderLayer(nn.Module):
                 memory_pos=None, self_attn_mask=None, cross_attn_mask=None):
         assert cross_attn_mask is None
         if self.self_attn is not None:
-            q = k = self.with_pos_embed(tgt, tgt_query_pos)
+            # q = k = tgt + pos with the bf16 twins of the sum and of tgt
+            # (the value) written in the same pass: the self-attention's
+            # packed in-projection reads them instead of two cast kernels
+            q = k = tgt if tgt_query_pos is None else add_with_twins(tgt, tgt_query_pos)
             tgt2 = self.self_attn(q, k, tgt, attn_mask=self_attn_mask)[0]
             if self.use_text_cross_attention:
                 # two handles (the text cross-attention's query, its residual)
@@ -541,7 +544,8 @@ class DeformableTransformerDecoderLayer(nn.Module):
             # two identical transposes): one object lets the MHA project them
             # with one GEMM
             text_kv = memory_text.transpose(0, 1)
-            tgt2 = self.ca_text(self.with_pos_embed(tgt_q, tgt_query_pos), text_kv, text_kv,
+            ca_q = tgt_q if tgt_query_pos is None else add_with_twins(tgt_q, tgt_query_pos)
+            tgt2 = self.ca_text(ca_q, text_kv, text_kv,
                                 key_padding_mask=text_attention_mask)[0]
             # two handles (the deformable attention's query, its residual)
             tgt_q, tgt = add_norm(self.catext_norm, tgt, self.catext_dropout(tgt2), taps=2)
