@@ -192,6 +192,17 @@ fin2)
   python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/fin2_steady_state.txt 2>&1 &&
   exit $rc1
   ;;
+benchab)
+  # the default of every round-6 A/B switch against its alternative, the
+  # driver's bench (checkpointing compare off) per setting
+  for sw in BASE GD_ATTN_SPLIT=0 GD_WATTN_BWD2=0 GD_ADDLN_V4=0 GD_TLIN=0 GD_WATTN_BLOCKS=2048 BASE2; do
+    step "bench with $sw"
+    case "$sw" in BASE*) e=() ;; *) e=("$sw") ;; esac
+    env "${e[@]}" timeout -k 10 300 python3 bench.py --no-cpu-baseline --ckpt-compare off --steps 20 --warmup 5 \
+        > "gpurun_out/benchab_${sw%%=*}.log" 2>&1 || exit $?
+    grep '^{' "gpurun_out/benchab_${sw%%=*}.log" | tail -1 | cut -c1-120
+  done
+  ;;
 lossab)
   # which round-6 kernel change moved cfg3's bf16 loss error: the full-size
   # gradient test under each A/B switch (one process per setting)
