@@ -605,11 +605,13 @@ extern "C" int gd_wgrad_splits_batched(int T, int O, int I, int batch) {
   // 128 tokens each: the fp32 partials (splits x O x I) stay a fraction of
   // the token-major inputs the kernel streams
   const int tiles = ((O + kTrTile - 1) / kTrTile) * ((I + kTrTile - 1) / kTrTile) * (batch > 0 ? batch : 1);
-  // 384 workgroups; 512 when a split has 16+ output tiles (FFN-sized weights,
-  // the batched BiAttention products): there the extra splits' partials cost
-  // less than the added loads in flight win (tools/wgrad_microbench.py,
-  // profiles/r04c_wgrad_ab.jsonl: enc FFN 88 -> 75 us, 256 x 256 worse)
-  const int wgs = target_wgs() > 0 ? target_wgs() : (tiles >= 16 ? 512 : 384);
+  // 256 workgroups (one per CU).  Round 4 picked 384 / 512 (512 for
+  // FFN-sized weights) from kernels timed alone (profiles/r04c_wgrad_ab.jsonl:
+  // enc FFN 88 -> 75 us); in the round-6 train step fewer splits -- less
+  // fp32 partial traffic and reduce work next to the other kernels -- won:
+  // 46.04 vs 45.76 images/s over three interleaved pairs and a separate run
+  // (profiles/r06i_knobs.txt; GD_WGRAD_WGS=384 / 512 / 768 / 1024 / 192 for A/B)
+  const int wgs = target_wgs() > 0 ? target_wgs() : 256;
   int s = tiles > 0 ? (wgs + tiles - 1) / tiles : 1;
   const int cap = T / 128 > 1 ? T / 128 : 1;
   return s < 1 ? 1 : (s > cap ? cap : s);

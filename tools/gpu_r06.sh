@@ -203,6 +203,17 @@ benchab)
     grep '^{' "gpurun_out/benchab_${sw%%=*}.log" | tail -1 | cut -c1-120
   done
   ;;
+knobs)
+  # the driver's bench (checkpointing compare off) under each NAME=VALUE
+  # given after the mode, BASE = the defaults
+  for sw in "${@:2}"; do
+    step "bench with $sw"
+    case "$sw" in BASE*) e=() ;; *) e=("$sw") ;; esac
+    env "${e[@]}" timeout -k 10 300 python3 bench.py --no-cpu-baseline --ckpt-compare off --steps 20 --warmup 5 \
+        > "gpurun_out/knobs_${sw//[=,]/_}.log" 2>&1 || exit $?
+    grep '^{' "gpurun_out/knobs_${sw//[=,]/_}.log" | tail -1 | cut -c60-130
+  done
+  ;;
 lossab)
   # which round-6 kernel change moved cfg3's bf16 loss error: the full-size
   # gradient test under each A/B switch (one process per setting)
