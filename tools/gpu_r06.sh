@@ -214,6 +214,25 @@ knobs)
     grep '^{' "gpurun_out/knobs_${sw//[=,]/_}.log" | tail -1 | cut -c60-130
   done
   ;;
+prof)
+  # the final build's rocprofv3 --stats trace and FETCH_SIZE / WRITE_SIZE
+  # passes of the bench step (one counter per run)
+  step "rocprof kernel trace" &&
+  T 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PROF/prof" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 4 --warmup 3 --ckpt-compare off > gpurun_out/prof_trace.log 2>&1 &&
+  mkdir -p gpurun_out/prof &&
+  find "$PROF/prof" -name '*stats*.csv' -exec cp {} gpurun_out/prof/ \; &&
+  kt=$(find "$PROF/prof" -name '*kernel_trace.csv' | head -n 1) &&
+  python3 tools/trace_steps.py --skip 2 "$kt" > gpurun_out/prof/steady_state.txt 2>&1 &&
+  step "pmc FETCH_SIZE" &&
+  T 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$PROF/prof_fetch" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --ckpt-compare off > gpurun_out/prof_fetch.log 2>&1 &&
+  step "pmc WRITE_SIZE" &&
+  T 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$PROF/prof_write" -o run -- \
+      python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --ckpt-compare off > gpurun_out/prof_write.log 2>&1 &&
+  python3 tools/pmc_traffic.py --fetch "$PROF/prof_fetch" --write "$PROF/prof_write" \
+      --out gpurun_out/prof_pmc_traffic.json > gpurun_out/prof_pmc_traffic.log 2>&1
+  ;;
 lossab)
   # which round-6 kernel change moved cfg3's bf16 loss error: the full-size
   # gradient test under each A/B switch (one process per setting)
